@@ -1,0 +1,219 @@
+"""Benchmark: Mrays/s of the MI355X ray tracer on BASELINE.json's config.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
+
+A step = one full pass of the hot path over one frame band: the prep, bin
+and trace kernels of librt_hip.so on a scene already resident in HBM,
+writing the int32x4 framebuffer band to HBM (rt_render_device).
+
+Workload at N=1 is BASELINE config 3: 4096x4096, 256 spheres + 64 cubes,
+dense synthetic scene (seed 3, k = 4096/640).  With N ranks
+the image grows to 4096 x (4096 N) with N x (256 + 64) primitives of the
+same density and rank r renders rows [4096 r, 4096 (r+1)): per-GPU work is
+fixed (weak scaling), no collective sits in the timed region.  The RCCL
+gather that assembles the frame on rank 0 (north_star's Texture assembly)
+is measured separately and reported under "gather".
+
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+REPO = Path(__file__).resolve().parent
+sys.path.insert(0, str(REPO))
+import __graft_entry__  # noqa: E402
+
+METRIC = "Mrays/sec (primary) at 4096×4096, 1/2/4/8 MI355X; % HBM-write roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec); 6.29 TB/s measured copy
+BYTES_PER_RAY = {"i32x4": 16, "rgba8": 4}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--width", type=int, default=4096)
+    ap.add_argument("--height", type=int, default=4096, help="rows per rank")
+    ap.add_argument("--spheres", type=int, default=256, help="per rank")
+    ap.add_argument("--cubes", type=int, default=64, help="per rank")
+    ap.add_argument("--seed", type=int, default=3)
+    ap.add_argument("--k", type=float, default=None, help="object scale (default width/640)")
+    ap.add_argument("--format", choices=sorted(BYTES_PER_RAY), default="i32x4")
+    ap.add_argument("--cpu-rows", type=int, default=16,
+                    help="CPU baseline samples every Nth row of rank 0's band")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--pmc", default=str(REPO / "profiles" / "r01_pmc_config3.json"),
+                    help="committed PMC summary to read `traffic` from")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and not (world == 1 and args.gpus == 1):
+        if world == 1:
+            raise SystemExit(f"--gpus {args.gpus} needs torchrun with {args.gpus} ranks")
+    distributed = world > 1
+    if distributed:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    pkg = __graft_entry__.load_package()
+    w, rows = args.width, args.height
+    full_h = rows * world
+    k = args.k if args.k is not None else w / 640.0
+    n_sph, n_cub = args.spheres * world, args.cubes * world
+    scene = pkg.Scene.synthetic(w, full_h, n_sph, n_cub, seed=args.seed, k=k)
+    rb, re = rank * rows, (rank + 1) * rows
+
+    rt = pkg.RayTracer(local)
+    t = {name: torch.from_numpy(np.ascontiguousarray(getattr(scene, name))).to(dev)
+         for name in ("sphere_origins", "sphere_radius", "sphere_colours", "cube_vertices",
+                      "cube_colours")}
+    dscene = {name: v.data_ptr() for name, v in t.items()}
+    dscene.update(num_spheres=scene.num_spheres, num_cubes=scene.num_cubes)
+    if args.format == "i32x4":
+        out = torch.empty((rows, w, 4), dtype=torch.int32, device=dev)
+    else:
+        out = torch.empty((rows, w), dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        rt.render_device(dscene, w, full_h, (rb, re), out.data_ptr(), fmt=args.format,
+                         stream=stream.cuda_stream)
+
+    def barrier():
+        if distributed:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    barrier()
+    torch.cuda.synchronize(dev)
+
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    barrier()
+    torch.cuda.synchronize(dev)
+    wall_ms = (time.perf_counter() - t0) * 1e3 / args.steps
+    event_ms = ev0.elapsed_time(ev1) / args.steps
+    if distributed:
+        tt = torch.tensor([wall_ms], device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        wall_ms = float(tt.item())
+
+    # Per-kernel durations: a second, profiled pass (HIP events on the launch
+    # stream between prep / bin / trace, inside librt_hip.so).
+    rt.profile(True)
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    prof = rt.profile_read()
+    rt.profile(False)
+    n = max(prof["renders"], 1)
+    trace_ms = prof["trace_ms"] / n
+    prep_ms, bin_ms = prof["prep_ms"] / n, prof["bin_ms"] / n
+
+    rays_rank = w * rows
+    value = world * rays_rank / (wall_ms * 1e-3) / 1e6
+    algo_bytes = BYTES_PER_RAY[args.format] * rays_rank
+    achieved = algo_bytes / (trace_ms * 1e-3) / 1e9
+
+    traffic = None
+    pmc_path = Path(args.pmc)
+    if pmc_path.exists():
+        try:
+            pmc = json.loads(pmc_path.read_text())
+            if pmc.get("config") == [w, rows, args.spheres, args.cubes, args.seed, args.format]:
+                traffic = pmc.get("hbm_bytes_per_launch")
+        except (ValueError, OSError):
+            traffic = None
+
+    gather = None
+    if distributed and not args.no_gather:
+        gl = [torch.empty_like(out) for _ in range(world)] if rank == 0 else None
+        for _ in range(2):
+            dist.gather(out, gl, dst=0)
+        torch.cuda.synchronize(dev)
+        barrier()
+        g0 = time.perf_counter()
+        reps = max(3, args.steps // 4)
+        for _ in range(reps):
+            dist.gather(out, gl, dst=0)
+        torch.cuda.synchronize(dev)
+        barrier()
+        g_ms = (time.perf_counter() - g0) * 1e3 / reps
+        gather = {"collective": "rccl gather to rank 0", "ms": g_ms,
+                  "bytes_to_root": algo_bytes * (world - 1),
+                  "render_plus_gather_mrays": world * rays_rank / ((wall_ms + g_ms) * 1e-3) / 1e6}
+
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        sys.path.insert(0, str(REPO / "tests"))
+        from oracle_lib import Oracle  # CPU baseline only
+
+        threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        orc = Oracle()
+        sample_rows = list(range(rb, re, args.cpu_rows))
+        c0 = time.perf_counter()
+        for r in sample_rows:
+            orc.trace(scene, w, full_h, rows=(r, r + 1), threads=threads)
+        c_s = time.perf_counter() - c0
+        cpu = {"value": len(sample_rows) * w / c_s / 1e6, "unit": "Mrays/s", "cores": threads,
+               "kind": "port",
+               "sample": f"{len(sample_rows)} rows (every {args.cpu_rows}th of rank 0's band) x {w}"
+                         f" px of the same scene, oracle/rt_oracle.c orc_trace_mt, {c_s:.1f} s"}
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(value, 1), "unit": "Mrays/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(wall_ms, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic",
+            "config": {"workload": f"config3: {w}x{rows} rows/rank, {args.spheres} spheres + "
+                                   f"{args.cubes} cubes per rank, dense k={k:.2f}, seed {args.seed}",
+                       "width": w, "rows_per_rank": rows, "image_height": full_h,
+                       "spheres": n_sph, "cubes": n_cub, "format": args.format,
+                       "parallelism": f"row-bands x{world}"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic, "kernel": "trace_kernel",
+                         "kernel_ms": round(trace_ms, 4), "prep_ms": round(prep_ms, 4),
+                         "bin_ms": round(bin_ms, 4), "algo_bytes_per_launch": algo_bytes},
+            "event_ms_per_step": round(event_ms, 4),
+            "cpu_baseline": cpu,
+            "gather": gather,
+        }
+        print(json.dumps(line), flush=True)
+    rt.close()
+    if distributed:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

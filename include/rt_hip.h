@@ -1,0 +1,174 @@
+/*
+ * rt_hip.h -- C ABI of the MI355X-native per-pixel ray tracer (librt_hip.so).
+ *
+ * Drop-in boundary for RichardHancock/OpenCL-Ray-Tracer's GPU trace path.
+ * Each entry point names the reference code it replaces (paths relative to
+ * /root/reference/RayTrace).  Plain pointers and sizes only; no HIP, torch or
+ * glm types cross this boundary.
+ *
+ * Scene layout is the reference's own flattened layout
+ * (MainState.cpp:646-658, MainState.h:99-106):
+ *   sphere_origins  float4[num_spheres]     (x, y, z, w)
+ *   sphere_radius   float [num_spheres]
+ *   sphere_colours  float4[num_spheres]     (r, g, b, a)
+ *   cube_vertices   float4[36 * num_cubes]  12 world-space triangles per cube
+ *   cube_colours    float4[num_cubes]
+ * Output frame (MainState.cpp:952-955, rayTracer.cl:198-201):
+ *   RT_FORMAT_I32X4: int32[rows][width][4], truncated (int) r, g, b, a
+ *   RT_FORMAT_RGBA8: uint32[rows][width], (uint8)r | (uint8)g<<8 |
+ *                    (uint8)b<<16 | 0xFF<<24  (the Texture packing,
+ *                    MainState.cpp:984-994, :1023-1037)
+ */
+#ifndef RT_HIP_H
+#define RT_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+/* Status codes: 0 = success, negative = failure.  Replaces the reference's
+ * print-and-continue cl_int handling (MainState.cpp:1101-1179 getErrorString,
+ * :672-674 etc.): the caller decides what to do. */
+enum {
+    RT_OK = 0,
+    RT_ERR_INVALID_ARG = -1,
+    RT_ERR_NO_DEVICE = -2,
+    RT_ERR_HIP = -3,
+    RT_ERR_OUT_OF_MEMORY = -4,
+    RT_ERR_UNSUPPORTED = -5
+};
+
+enum { RT_FORMAT_I32X4 = 0, RT_FORMAT_RGBA8 = 1 };
+
+/* Kernel path selection (rt_render*, `path` field of rt_timing). */
+enum {
+    RT_PATH_AUTO = 0,    /* binned when its preconditions hold, else generic */
+    RT_PATH_BINNED = 1,  /* implicit origins (x,y,0,1), ray_dir = (0,0,D,w) */
+    RT_PATH_GENERIC = 2  /* any origins / direction, brute force per pixel */
+};
+
+typedef struct rt_scene {
+    const float* sphere_origins;
+    const float* sphere_radius;
+    const float* sphere_colours;
+    int32_t num_spheres;
+    const float* cube_vertices;
+    const float* cube_colours;
+    int32_t num_cubes;
+    /* float4[num_lights].  Carried for ABI completeness; the reference has no
+     * lighting model (its "shade" is a depth ramp, MainState.cpp:396-407), so
+     * lights never change the output. */
+    const float* lights;
+    int32_t num_lights;
+} rt_scene;
+
+typedef struct rt_timing {
+    double total_us;    /* host wall time of the whole call (the reference's
+                           timer scope, MainState.cpp:662-894) */
+    double upload_us;   /* H2D scene (+ origins) copy, HIP events */
+    double kernel_us;   /* all render kernels, HIP events */
+    double download_us; /* D2H frame copy, HIP events */
+    int32_t path;       /* RT_PATH_BINNED or RT_PATH_GENERIC actually used */
+} rt_timing;
+
+typedef struct rt_ctx rt_ctx;
+
+/* Replaces MainState::openCLInit (MainState.cpp:1181-1326): selects HIP
+ * device `device_ordinal`, creates the stream and the workspace.  One
+ * context per device; not re-entrant per context. */
+int rt_init(int device_ordinal, rt_ctx** out_ctx);
+
+/* Releases everything rt_init / rt_render allocated (MainState.cpp:73-78). */
+void rt_destroy(rt_ctx* ctx);
+
+/* Replaces MainState::getErrorString (MainState.cpp:1101-1179). */
+const char* rt_error_string(int status);
+
+/* Replaces the body of MainState::executeRayTracerOpenCL
+ * (MainState.cpp:641-934): buffer setup, the six scene/ray uploads, the
+ * clEnqueueNDRangeKernel launch of rayTracer.cl::rayTracer and the blocking
+ * map/readback.  Synchronous: on return `host_out` holds rows
+ * [row_begin, row_end) of the width x height frame.
+ *   ray_dir       float4, the reference passes (0,0,-1,-1) (MainState.cpp:37-39)
+ *   ray_origins   NULL for the reference's implicit (x, y, 0, 1) grid
+ *                 (MainState.cpp:44-50), else float4[width*height] (full frame)
+ *   host_out      int32[4*width*rows] (I32X4) or uint32[width*rows] (RGBA8)
+ *   timing        may be NULL
+ * Empty scenes are legal (all pixels (0,0,0,255)). */
+int rt_render(rt_ctx* ctx, const rt_scene* scene, const float ray_dir[4],
+              const float* ray_origins, int32_t width, int32_t height,
+              int32_t row_begin, int32_t row_end, int32_t out_format,
+              void* host_out, rt_timing* timing);
+
+/* Same as rt_render with an explicit path (RT_PATH_*).  RT_PATH_BINNED
+ * returns RT_ERR_UNSUPPORTED when its preconditions do not hold. */
+int rt_render_path(rt_ctx* ctx, const rt_scene* scene, const float ray_dir[4],
+                   const float* ray_origins, int32_t width, int32_t height,
+                   int32_t row_begin, int32_t row_end, int32_t out_format,
+                   int32_t path, void* host_out, rt_timing* timing);
+
+/* Device-resident variant (no reference counterpart; used by the multi-GPU
+ * row-band driver and the benchmark): every pointer in `device_scene`,
+ * `device_ray_origins` and `device_out` is a device pointer on the context's
+ * device, `stream` is a hipStream_t (NULL = the context's stream).
+ * Asynchronous: work is enqueued on `stream` and the call returns. */
+int rt_render_device(rt_ctx* ctx, const rt_scene* device_scene,
+                     const float ray_dir[4], const float* device_ray_origins,
+                     int32_t width, int32_t height, int32_t row_begin,
+                     int32_t row_end, int32_t out_format, int32_t path,
+                     void* device_out, void* stream);
+
+/* Per-kernel HIP-event profiling of rt_render_device / rt_render launches.
+ * rt_profile_enable(ctx, 1) starts recording; rt_profile_read synchronises,
+ * returns the summed milliseconds of the prep, bin and trace kernels and the
+ * number of renders recorded, then resets the accumulators. */
+int rt_profile_enable(rt_ctx* ctx, int enable);
+int rt_profile_read(rt_ctx* ctx, double* prep_ms, double* bin_ms,
+                    double* trace_ms, int32_t* n_renders);
+
+/* Device facts for reporting (HBM bytes, CU count, name). */
+int rt_device_info(rt_ctx* ctx, char* name, int32_t name_len, int32_t* n_cu,
+                   int64_t* total_mem);
+
+/* ---- host-side scene helpers (no GPU needed) ------------------------- */
+
+/* Cube, Cube.cpp:6-83: unit cube, scale, rotate (Rz*Ry*Rx, radians),
+ * translate, in place on float4[36]. */
+void rt_cube_init(float vertices[144]);
+void rt_cube_scale(float vertices[144], float sx, float sy, float sz);
+void rt_cube_rotate(float vertices[144], float rx, float ry, float rz);
+void rt_cube_translate(float vertices[144], float tx, float ty, float tz);
+/* Utility::convertAngleToRadian, Utility.cpp:343-347 */
+float rt_deg_to_rad(float degrees);
+/* rayDir = perspective(45, 4/3, 0, 100) * (0,0,1,1), MainState.cpp:37-39 */
+void rt_primary_ray_dir(float out[4]);
+
+/* MainState::createScene1/2/3 (MainState.cpp:419-639) into caller arrays of
+ * capacity 100 spheres / 100 cubes; Random::init(seed) = srand(seed). */
+int rt_scene_reference(int32_t scene_id, uint32_t seed, float* sphere_origins,
+                       float* sphere_radius, float* sphere_colours,
+                       float* cube_vertices, float* cube_colours,
+                       int32_t* num_spheres, int32_t* num_cubes);
+
+/* Synthetic N-sphere / M-cube scene (SURVEY.md §8d distributions, seeded
+ * splitmix64, object scale k: 1 = sparse, width/640 = dense). */
+int rt_scene_synthetic(int32_t width, int32_t height, int32_t num_spheres,
+                       int32_t num_cubes, uint64_t seed, float k,
+                       float* sphere_origins, float* sphere_radius,
+                       float* sphere_colours, float* cube_vertices,
+                       float* cube_colours);
+
+/* Texture conversion (MainState.cpp:1023-1037) on the host. */
+void rt_pack_rgba8(const int32_t* frame, int64_t n_pixels, uint32_t* out);
+
+/* Library / ABI version. */
+int rt_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RT_HIP_H */

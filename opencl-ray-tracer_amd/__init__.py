@@ -1,0 +1,394 @@
+"""opencl-ray-tracer_amd -- Python host mirror of the MI355X ray tracer's C ABI.
+
+The product is ``librt_hip.so`` (``csrc/``, declared in ``include/rt_hip.h``):
+the HIP kernels plus the C ABI that replaces the reference's OpenCL dispatch
+``MainState::executeRayTracerOpenCL`` (RayTrace/states/MainState.cpp:641-934).
+This module binds that library with ctypes and mirrors the reference's
+call-site vocabulary (``MainState`` with ``createScene1..3`` and
+``executeRayTracer``), so tests and the benchmark read like the reference's
+own control flow.  There is no CPU fallback here: if the library or a GPU is
+missing, calls raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass, field
+from pathlib import Path
+from typing import Optional, Tuple
+
+import numpy as np
+
+__all__ = [
+    "RT_OK", "RT_FORMAT_I32X4", "RT_FORMAT_RGBA8", "RT_PATH_AUTO", "RT_PATH_BINNED",
+    "RT_PATH_GENERIC", "RtError", "Scene", "Timing", "RayTracer", "MainState",
+    "library", "library_path", "primary_ray_dir", "pack_rgba8", "cube_packed",
+    "deg_to_rad", "EXPORTED_SYMBOLS",
+]
+
+PKG_DIR = Path(__file__).resolve().parent
+RT_OK = 0
+RT_FORMAT_I32X4, RT_FORMAT_RGBA8 = 0, 1
+RT_PATH_AUTO, RT_PATH_BINNED, RT_PATH_GENERIC = 0, 1, 2
+_FORMATS = {"i32x4": RT_FORMAT_I32X4, "rgba8": RT_FORMAT_RGBA8}
+_PATHS = {"auto": RT_PATH_AUTO, "binned": RT_PATH_BINNED, "generic": RT_PATH_GENERIC}
+
+# Every symbol include/rt_hip.h declares (tests check the .so exports them).
+EXPORTED_SYMBOLS = (
+    "rt_init", "rt_destroy", "rt_error_string", "rt_render", "rt_render_path",
+    "rt_render_device", "rt_profile_enable", "rt_profile_read", "rt_device_info",
+    "rt_cube_init", "rt_cube_scale", "rt_cube_rotate", "rt_cube_translate",
+    "rt_deg_to_rad", "rt_primary_ray_dir", "rt_scene_reference", "rt_scene_synthetic",
+    "rt_pack_rgba8", "rt_abi_version",
+)
+
+
+class RtError(RuntimeError):
+    """A negative status from librt_hip.so (rt_error_string text attached)."""
+
+    def __init__(self, status: int, what: str):
+        self.status = status
+        super().__init__(f"{what}: {_error_string(status)} ({status})")
+
+
+class _Scene(ctypes.Structure):
+    _fields_ = [
+        ("sphere_origins", ctypes.c_void_p), ("sphere_radius", ctypes.c_void_p),
+        ("sphere_colours", ctypes.c_void_p), ("num_spheres", ctypes.c_int32),
+        ("cube_vertices", ctypes.c_void_p), ("cube_colours", ctypes.c_void_p),
+        ("num_cubes", ctypes.c_int32), ("lights", ctypes.c_void_p),
+        ("num_lights", ctypes.c_int32),
+    ]
+
+
+class _Timing(ctypes.Structure):
+    _fields_ = [
+        ("total_us", ctypes.c_double), ("upload_us", ctypes.c_double),
+        ("kernel_us", ctypes.c_double), ("download_us", ctypes.c_double),
+        ("path", ctypes.c_int32),
+    ]
+
+
+_LIB: Optional[ctypes.CDLL] = None
+
+
+def library_path() -> Path:
+    return Path(os.environ.get("RT_HIP_LIBRARY", PKG_DIR / "librt_hip.so"))
+
+
+def library() -> ctypes.CDLL:
+    """Load librt_hip.so (built by ``make -C csrc`` / ``__graft_entry__.build``)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    path = library_path()
+    if not path.exists():
+        raise RuntimeError(f"{path} is missing: build it with `make -C {PKG_DIR / 'csrc'}`")
+    lib = ctypes.CDLL(str(path))
+    vp, i32, f32 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_float
+    sig = {
+        "rt_init": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(vp)]),
+        "rt_destroy": (None, [vp]),
+        "rt_error_string": (ctypes.c_char_p, [ctypes.c_int]),
+        "rt_render": (ctypes.c_int, [vp, ctypes.POINTER(_Scene), vp, vp, i32, i32, i32, i32,
+                                     i32, vp, ctypes.POINTER(_Timing)]),
+        "rt_render_path": (ctypes.c_int, [vp, ctypes.POINTER(_Scene), vp, vp, i32, i32, i32,
+                                          i32, i32, i32, vp, ctypes.POINTER(_Timing)]),
+        "rt_render_device": (ctypes.c_int, [vp, ctypes.POINTER(_Scene), vp, vp, i32, i32, i32,
+                                            i32, i32, i32, vp, vp]),
+        "rt_profile_enable": (ctypes.c_int, [vp, ctypes.c_int]),
+        "rt_profile_read": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double),
+                                           ctypes.POINTER(ctypes.c_double),
+                                           ctypes.POINTER(ctypes.c_double),
+                                           ctypes.POINTER(i32)]),
+        "rt_device_info": (ctypes.c_int, [vp, ctypes.c_char_p, i32, ctypes.POINTER(i32),
+                                          ctypes.POINTER(ctypes.c_int64)]),
+        "rt_cube_init": (None, [vp]),
+        "rt_cube_scale": (None, [vp, f32, f32, f32]),
+        "rt_cube_rotate": (None, [vp, f32, f32, f32]),
+        "rt_cube_translate": (None, [vp, f32, f32, f32]),
+        "rt_deg_to_rad": (f32, [f32]),
+        "rt_primary_ray_dir": (None, [vp]),
+        "rt_scene_reference": (ctypes.c_int, [i32, ctypes.c_uint32, vp, vp, vp, vp, vp,
+                                              ctypes.POINTER(i32), ctypes.POINTER(i32)]),
+        "rt_scene_synthetic": (ctypes.c_int, [i32, i32, i32, i32, ctypes.c_uint64, f32, vp,
+                                              vp, vp, vp, vp]),
+        "rt_pack_rgba8": (None, [vp, ctypes.c_int64, vp]),
+        "rt_abi_version": (ctypes.c_int, []),
+        "rt_selftest_fp32": (ctypes.c_int, [vp, vp, i32, vp, vp]),
+        "rt_debug_triangle_box": (ctypes.c_int, [vp, vp, vp, vp, i32, i32, i32, vp]),
+        "rt_debug_sphere_box": (ctypes.c_int, [vp, f32, vp, i32, i32, i32, vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _LIB = lib
+    return lib
+
+
+def _error_string(status: int) -> str:
+    try:
+        return library().rt_error_string(status).decode()
+    except Exception:  # pragma: no cover - library missing while formatting
+        return "unknown"
+
+
+def _ptr(a: Optional[np.ndarray]) -> Optional[int]:
+    return None if a is None else a.ctypes.data
+
+
+def _check(status: int, what: str) -> None:
+    if status != RT_OK:
+        raise RtError(status, what)
+
+
+# ---------------------------------------------------------------------------
+# host-side scene helpers (Cube.cpp, Utility.cpp, MainState.cpp:37-39)
+# ---------------------------------------------------------------------------
+def deg_to_rad(deg: float) -> float:
+    return float(library().rt_deg_to_rad(deg))
+
+
+def primary_ray_dir() -> np.ndarray:
+    out = np.zeros(4, np.float32)
+    library().rt_primary_ray_dir(_ptr(out))
+    return out
+
+
+def cube_packed(ops) -> np.ndarray:
+    """Unit cube transformed by ops [("scale"|"rotate"|"translate", x, y, z), ...]."""
+    lib = library()
+    v = np.zeros((36, 4), np.float32)
+    lib.rt_cube_init(_ptr(v))
+    fns = {"scale": lib.rt_cube_scale, "rotate": lib.rt_cube_rotate,
+           "translate": lib.rt_cube_translate}
+    for op, x, y, z in ops:
+        fns[op](_ptr(v), x, y, z)
+    return v
+
+
+def pack_rgba8(frame: np.ndarray) -> np.ndarray:
+    """Texture conversion (MainState.cpp:1023-1037) of an int32x4 frame."""
+    frame = np.ascontiguousarray(frame, dtype=np.int32)
+    n = frame.size // 4
+    out = np.zeros(frame.shape[:-1], np.uint32)
+    library().rt_pack_rgba8(_ptr(frame), n, _ptr(out))
+    return out
+
+
+@dataclass
+class Scene:
+    """The reference's scene vectors (MainState.h:99-106), cubes flattened
+    to 36 world-space float4 vertices each (MainState.cpp:646-655)."""
+
+    sphere_origins: np.ndarray = field(default_factory=lambda: np.zeros((0, 4), np.float32))
+    sphere_radius: np.ndarray = field(default_factory=lambda: np.zeros((0,), np.float32))
+    sphere_colours: np.ndarray = field(default_factory=lambda: np.zeros((0, 4), np.float32))
+    cube_vertices: np.ndarray = field(default_factory=lambda: np.zeros((0, 36, 4), np.float32))
+    cube_colours: np.ndarray = field(default_factory=lambda: np.zeros((0, 4), np.float32))
+    lights: np.ndarray = field(default_factory=lambda: np.zeros((0, 4), np.float32))
+
+    def __post_init__(self):
+        self.sphere_origins = np.ascontiguousarray(self.sphere_origins, np.float32).reshape(-1, 4)
+        self.sphere_radius = np.ascontiguousarray(self.sphere_radius, np.float32).reshape(-1)
+        self.sphere_colours = np.ascontiguousarray(self.sphere_colours, np.float32).reshape(-1, 4)
+        self.cube_vertices = np.ascontiguousarray(self.cube_vertices, np.float32).reshape(-1, 36, 4)
+        self.cube_colours = np.ascontiguousarray(self.cube_colours, np.float32).reshape(-1, 4)
+        self.lights = np.ascontiguousarray(self.lights, np.float32).reshape(-1, 4)
+        if not (len(self.sphere_origins) == len(self.sphere_radius) == len(self.sphere_colours)):
+            raise ValueError("sphere arrays disagree in length")
+        if len(self.cube_vertices) != len(self.cube_colours):
+            raise ValueError("cube arrays disagree in length")
+
+    @property
+    def num_spheres(self) -> int:
+        return len(self.sphere_radius)
+
+    @property
+    def num_cubes(self) -> int:
+        return len(self.cube_colours)
+
+    def as_c(self) -> _Scene:
+        return _Scene(_ptr(self.sphere_origins), _ptr(self.sphere_radius),
+                      _ptr(self.sphere_colours), self.num_spheres, _ptr(self.cube_vertices),
+                      _ptr(self.cube_colours), self.num_cubes, _ptr(self.lights),
+                      len(self.lights))
+
+    @classmethod
+    def reference(cls, scene_id: int, seed: int = 1) -> "Scene":
+        """MainState::createScene1/2/3 (MainState.cpp:419-639) after
+        Random::init(seed)."""
+        so = np.zeros((100, 4), np.float32)
+        sr = np.zeros(100, np.float32)
+        sc = np.zeros((100, 4), np.float32)
+        cv = np.zeros((100, 36, 4), np.float32)
+        cc = np.zeros((100, 4), np.float32)
+        ns, nc = ctypes.c_int32(), ctypes.c_int32()
+        _check(library().rt_scene_reference(scene_id, seed, _ptr(so), _ptr(sr), _ptr(sc),
+                                            _ptr(cv), _ptr(cc), ctypes.byref(ns),
+                                            ctypes.byref(nc)), "rt_scene_reference")
+        return cls(so[:ns.value], sr[:ns.value], sc[:ns.value], cv[:nc.value], cc[:nc.value])
+
+    @classmethod
+    def synthetic(cls, width: int, height: int, n_spheres: int, n_cubes: int,
+                  seed: int = 7, k: float = 1.0, n_lights: int = 0) -> "Scene":
+        """SURVEY.md §8d synthetic N-sphere/M-cube scene; lights are carried
+        (the reference has no lighting model, so they never change pixels)."""
+        so = np.zeros((n_spheres, 4), np.float32)
+        sr = np.zeros(n_spheres, np.float32)
+        sc = np.zeros((n_spheres, 4), np.float32)
+        cv = np.zeros((n_cubes, 36, 4), np.float32)
+        cc = np.zeros((n_cubes, 4), np.float32)
+        _check(library().rt_scene_synthetic(width, height, n_spheres, n_cubes, seed, k,
+                                            _ptr(so), _ptr(sr), _ptr(sc), _ptr(cv), _ptr(cc)),
+               "rt_scene_synthetic")
+        lights = np.tile(np.array([[width / 2, height / 2, 200.0, 1.0]], np.float32),
+                         (n_lights, 1))
+        return cls(so, sr, sc, cv, cc, lights)
+
+
+@dataclass
+class Timing:
+    total_us: float
+    upload_us: float
+    kernel_us: float
+    download_us: float
+    path: str
+
+
+class RayTracer:
+    """One HIP device context (rt_init / rt_destroy)."""
+
+    def __init__(self, device: int = 0):
+        lib = library()
+        self._ctx = ctypes.c_void_p()
+        _check(lib.rt_init(device, ctypes.byref(self._ctx)), "rt_init")
+        self.device = device
+
+    def close(self) -> None:
+        if self._ctx:
+            library().rt_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):  # pragma: no cover - interpreter teardown order
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self) -> ctypes.c_void_p:
+        return self._ctx
+
+    def render(self, scene: Scene, width: int, height: int, rows: Optional[Tuple[int, int]] = None,
+               ray_dir: Optional[np.ndarray] = None, ray_origins: Optional[np.ndarray] = None,
+               fmt: str = "i32x4", path: str = "auto") -> Tuple[np.ndarray, Timing]:
+        """Synchronous host-buffer render (rt_render_path).  Returns the frame
+        (rows x width x 4 int32, or rows x width uint32 for rgba8)."""
+        rb, re = rows if rows is not None else (0, height)
+        d = primary_ray_dir() if ray_dir is None else np.ascontiguousarray(ray_dir, np.float32)
+        org = None if ray_origins is None else np.ascontiguousarray(ray_origins, np.float32)
+        if org is not None and org.size != 4 * width * height:
+            raise ValueError("ray_origins must hold width*height float4")
+        shape = (re - rb, width, 4) if fmt == "i32x4" else (re - rb, width)
+        out = np.empty(shape, np.int32 if fmt == "i32x4" else np.uint32)
+        t = _Timing()
+        sc = scene.as_c()
+        _check(library().rt_render_path(self._ctx, ctypes.byref(sc), _ptr(d), _ptr(org), width,
+                                        height, rb, re, _FORMATS[fmt], _PATHS[path], _ptr(out),
+                                        ctypes.byref(t)), "rt_render")
+        used = {RT_PATH_BINNED: "binned", RT_PATH_GENERIC: "generic"}.get(t.path, "?")
+        return out, Timing(t.total_us, t.upload_us, t.kernel_us, t.download_us, used)
+
+    def render_device(self, device_scene: dict, width: int, height: int, rows: Tuple[int, int],
+                      out_ptr: int, ray_dir: Optional[np.ndarray] = None, fmt: str = "i32x4",
+                      path: str = "auto", stream: int = 0, origins_ptr: int = 0) -> None:
+        """Asynchronous device-pointer render (rt_render_device).  `device_scene`
+        maps the rt_scene fields to device addresses (e.g. torch data_ptr())."""
+        d = primary_ray_dir() if ray_dir is None else np.ascontiguousarray(ray_dir, np.float32)
+        sc = _Scene(device_scene.get("sphere_origins"), device_scene.get("sphere_radius"),
+                    device_scene.get("sphere_colours"), int(device_scene.get("num_spheres", 0)),
+                    device_scene.get("cube_vertices"), device_scene.get("cube_colours"),
+                    int(device_scene.get("num_cubes", 0)), None, 0)
+        _check(library().rt_render_device(self._ctx, ctypes.byref(sc), _ptr(d),
+                                          origins_ptr or None, width, height, rows[0], rows[1],
+                                          _FORMATS[fmt], _PATHS[path], out_ptr, stream or None),
+               "rt_render_device")
+
+    def profile(self, enable: bool) -> None:
+        _check(library().rt_profile_enable(self._ctx, int(enable)), "rt_profile_enable")
+
+    def profile_read(self) -> dict:
+        a, b, c = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        n = ctypes.c_int32()
+        _check(library().rt_profile_read(self._ctx, ctypes.byref(a), ctypes.byref(b),
+                                         ctypes.byref(c), ctypes.byref(n)), "rt_profile_read")
+        return {"prep_ms": a.value, "bin_ms": b.value, "trace_ms": c.value, "renders": n.value}
+
+    def device_info(self) -> dict:
+        name = ctypes.create_string_buffer(256)
+        cu, mem = ctypes.c_int32(), ctypes.c_int64()
+        _check(library().rt_device_info(self._ctx, name, 256, ctypes.byref(cu),
+                                        ctypes.byref(mem)), "rt_device_info")
+        return {"name": name.value.decode(), "cus": cu.value, "total_mem": mem.value}
+
+    def selftest_fp32(self, x: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+        x = np.ascontiguousarray(x, np.float32)
+        s, q = np.empty_like(x), np.empty_like(x)
+        _check(library().rt_selftest_fp32(self._ctx, _ptr(x), x.size, _ptr(s), _ptr(q)),
+               "rt_selftest_fp32")
+        return s, q
+
+
+class MainState:
+    """Headless mirror of the reference's MainState trace flow
+    (MainState.cpp:135-239 update, :419-639 scenes, :641 executeRayTracerOpenCL).
+
+    ``execute_ray_tracer()`` leaves the int32x4 frame in ``pixels`` (a flat
+    int32 array of 4*W*H, as the reference's std::vector<int>) and the wall
+    time in ``time_taken`` (µs, the reference's timer scope :662-894)."""
+
+    def __init__(self, width: int = 640, height: int = 480, device: int = 0):
+        self.width, self.height = width, height
+        self.pixel_count = width * height  # :34
+        self.ray_dir = primary_ray_dir()   # :37-39
+        self.current_scene = 1
+        self.scene = Scene()
+        self.pixels = np.zeros(0, np.int32)
+        self.time_taken = 0.0
+        self._rt = RayTracer(device)       # openCLInit, :52
+
+    def create_scene(self, scene_id: int, seed: int = 1) -> None:
+        self.current_scene = scene_id
+        self.scene = Scene.reference(scene_id, seed)
+
+    def createScene1(self, seed: int = 1):  # noqa: N802 - reference names
+        self.create_scene(1, seed)
+
+    def createScene2(self, seed: int = 1):  # noqa: N802
+        self.create_scene(2, seed)
+
+    def createScene3(self, seed: int = 1):  # noqa: N802
+        self.create_scene(3, seed)
+
+    def execute_ray_tracer(self) -> np.ndarray:
+        frame, t = self._rt.render(self.scene, self.width, self.height, ray_dir=self.ray_dir)
+        self.pixels = frame.reshape(-1)
+        self.time_taken = t.total_us
+        return frame
+
+    executeRayTracerOpenCL = execute_ray_tracer  # noqa: N815 - the replaced entry
+
+    def generate_image_from_pixels(self) -> np.ndarray:
+        """RGBA8 Texture content (MainState.cpp:974-1045)."""
+        return pack_rgba8(self.pixels.reshape(self.height, self.width, 4))
+
+    def close(self):
+        self._rt.close()

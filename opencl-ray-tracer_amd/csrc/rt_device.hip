@@ -1,0 +1,893 @@
+// rt_device.hip -- MI355X (gfx950) ray-tracing kernels and the C ABI.
+//
+// Replaces the reference's OpenCL kernel rayTracer.cl::rayTracer
+// (RayTrace/resources/shaders/rayTracer.cl:111-202) and its host dispatch
+// MainState::executeRayTracerOpenCL (RayTrace/states/MainState.cpp:641-934).
+// The numerics follow the reference's serial CPU path (MainState.cpp:257-408):
+// fp64 Moller-Trumbore for cube triangles, fp32 glm sphere test, strict '<'
+// closest hit in cubes-then-spheres order, depth-ramp shade, (int) stores.
+//
+// Three kernels per frame (DESIGN.md "Kernels"):
+//   prep   one lane per primitive: per-triangle fp64 constants, per-sphere
+//          fp32 constants, and a conservative integer pixel box outside of
+//          which the exact test provably rejects.
+//   bin    one lane per (64-primitive word, 32x32 bin): ordered candidate
+//          bitmasks, bit order = the reference's primitive order.
+//   trace  one 256-thread workgroup per bin, one 16x16 tile per wave, four
+//          pixels per lane; wave-uniform candidate loop on scalar loads,
+//          exact per-lane tests, 16-B coalesced framebuffer stores.
+// Plus `generic`, a brute-force per-pixel kernel for arbitrary ray origins
+// and directions (the reference's kernel arguments 8-9 in full generality).
+//
+// Build: -ffp-contract=off (and the pragma below): every operation rounds
+// once, as x86-64 SSE does in the reference's CPU build.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "rt_hip.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+constexpr int kBinW = 32;         // bin = workgroup tile, pixels
+constexpr int kBinH = 32;
+constexpr int kWaveTile = 16;     // each wave owns a 16x16 quadrant of the bin
+constexpr int kRowsPerLane = 4;   // lane rows y0, y0+4, y0+8, y0+12
+constexpr int kThreads = 256;
+constexpr double kEpsilon = 0.000001;      // MainState.cpp:15
+constexpr float kFar = 300000.0f;          // MainState.cpp:345
+
+typedef int int4v __attribute__((ext_vector_type(4)));
+
+// Per-triangle constants of the binned path (128 B, scalar-loaded).
+// With implicit origins (x, y, 0) and dir = (0, 0, D): pvec = d x e2 and
+// det, inv_det are per-triangle; tvec = (x - v0x, y - v0y, -v0z) varies only
+// in x and y.  Every field is produced by the same fp64 operation sequence as
+// MainState.cpp:257-298, so per-pixel results are bit-identical.
+struct alignas(16) TriRec {
+    double v0x, v0y, p0, p1;
+    double inv_det, e1x, e1y, e1z;
+    double e2x, e2y, e2z, k0;  // k0 = tz * e1y
+    double k1, dz, pad0, pad1; // k1 = tz * e1x, dz = D
+};
+static_assert(sizeof(TriRec) == 128, "TriRec layout");
+
+// Per-sphere constants of the binned path (32 B).  With dir = (0, 0, D, Dw)
+// and origins (x, y, 0, 1): tca = dot4(L, d) and the z/w half of dot4(L, L)
+// do not depend on the pixel (MainState.cpp:300-327, glm pairwise dot).
+struct alignas(16) SphRec {
+    float cx, cy, kzw, tca2;  // kzw = Lz*Lz + Lw*Lw, tca2 = tca*tca
+    float r2, tca, pad0, pad1;
+};
+static_assert(sizeof(SphRec) == 32, "SphRec layout");
+
+struct Box { int x0, y0, x1, y1; };  // inclusive pixel range, empty if x0 > x1
+
+__host__ __device__ inline Box empty_box() { return Box{1, 1, 0, 0}; }
+
+__host__ __device__ inline bool finite3(double a, double b, double c) {
+    return std::isfinite(a) && std::isfinite(b) && std::isfinite(c);
+}
+
+__host__ __device__ inline int clamp_floor(double v, int lo, int hi) {
+    if (!(v > (double)lo)) return lo;
+    if (!(v < (double)hi)) return hi;
+    return (int)floor(v);
+}
+__host__ __device__ inline int clamp_ceil(double v, int lo, int hi) {
+    if (!(v > (double)lo)) return lo;
+    if (!(v < (double)hi)) return hi;
+    return (int)ceil(v);
+}
+
+// Triangle prep.  Returns false when the triangle can never report a hit in
+// the reference (|det| < EPSILON or a NaN det).  The box bound: outside the
+// triangle's xy box by a distance Dist, the exact barycentric minimum is
+// <= -Dist / (2 * extent); the computed u, v differ from the exact ones by
+// at most `err` (rounding of e1, e2, pvec, det, tvec and the products), so
+// a pad of 2 * extent * (2 * err + slack) (here x4 more) guarantees that
+// the computed test rejects.  Ill-conditioned dets get the whole band.
+__host__ __device__ inline bool prep_triangle(const float* a, const float* b, const float* c,
+                                              double dx, double dy, double dz, int width,
+                                              int row_begin, int row_end, TriRec* rec,
+                                              Box* box, bool* nonfinite) {
+    const double v0[3] = {a[0], a[1], a[2]};
+    const double v1[3] = {b[0], b[1], b[2]};
+    const double v2[3] = {c[0], c[1], c[2]};
+    *nonfinite = !(finite3(v0[0], v0[1], v0[2]) && finite3(v1[0], v1[1], v1[2]) &&
+                   finite3(v2[0], v2[1], v2[2]));
+    const double e1[3] = {v1[0] - v0[0], v1[1] - v0[1], v1[2] - v0[2]};
+    const double e2[3] = {v2[0] - v0[0], v2[1] - v0[1], v2[2] - v0[2]};
+    const double p0 = dy * e2[2] - dz * e2[1];
+    const double p1 = dz * e2[0] - dx * e2[2];
+    const double p2 = dx * e2[1] - dy * e2[0];
+    const double det = e1[0] * p0 + e1[1] * p1 + e1[2] * p2;
+    *box = empty_box();
+    if ((det > -kEpsilon && det < kEpsilon) || !(det == det) || *nonfinite) return false;
+    const double inv_det = 1.0 / det;
+    const double tz = 0.0 - v0[2];
+    rec->v0x = v0[0];
+    rec->v0y = v0[1];
+    rec->p0 = p0;
+    rec->p1 = p1;
+    rec->inv_det = inv_det;
+    rec->e1x = e1[0];
+    rec->e1y = e1[1];
+    rec->e1z = e1[2];
+    rec->e2x = e2[0];
+    rec->e2y = e2[1];
+    rec->e2z = e2[2];
+    rec->k0 = tz * e1[1];
+    rec->k1 = tz * e1[0];
+    rec->dz = dz;
+    rec->pad0 = rec->pad1 = 0.0;
+
+    const double eps = 1.1102230246251565e-16;  // 2^-53
+    const double mnx = fmin(v0[0], fmin(v1[0], v2[0])), mxx = fmax(v0[0], fmax(v1[0], v2[0]));
+    const double mny = fmin(v0[1], fmin(v1[1], v2[1])), mxy = fmax(v0[1], fmax(v1[1], v2[1]));
+    const double tx_max = fmax(fabs(0.0 - v0[0]), fabs((double)(width - 1) - v0[0])) + 1.0;
+    const double ty_max =
+        fmax(fabs((double)row_begin - v0[1]), fabs((double)(row_end - 1) - v0[1])) + 1.0;
+    const double adet = fabs(det);
+    const double rho =
+        8.0 * eps * (fabs(e1[0] * p0) + fabs(e1[1] * p1) + fabs(e1[2] * p2)) / adet + 4.0 * eps;
+    Box bx{0, row_begin, width - 1, row_end - 1};
+    if (rho < 0.25) {
+        const double s = (tx_max * (fabs(p0) + fabs(e1[1] * dz)) +
+                          ty_max * (fabs(p1) + fabs(e1[0] * dz))) * fabs(inv_det);
+        const double err = (32.0 * eps + 4.0 * rho) * s + 32.0 * eps;
+        const double g = 2.0 * err + 8.0 * eps * s + 32.0 * eps;
+        const double padx = 8.0 * (mxx - mnx) * g + 0.5;
+        const double pady = 8.0 * (mxy - mny) * g + 0.5;
+        bx.x0 = clamp_floor(mnx - padx, 0, width - 1);
+        bx.x1 = clamp_ceil(mxx + padx, 0, width - 1);
+        bx.y0 = clamp_floor(mny - pady, row_begin, row_end - 1);
+        bx.y1 = clamp_ceil(mxy + pady, row_begin, row_end - 1);
+        // wholly outside the band / frame?
+        if (mxx + padx < 0.0 || mnx - padx > (double)(width - 1) ||
+            mxy + pady < (double)row_begin || mny - pady > (double)(row_end - 1))
+            return true;  // box stays empty
+    }
+    *box = bx;
+    return true;
+}
+
+// Sphere prep (fp32, MainState.cpp:300-327 with glm's pairwise vec4 dot).
+// Miss is guaranteed where |L|^2 (1 - 8e) > r2 - (kzw - tca2) + 8e(|kzw| +
+// |tca2|), e = 2^-23 (bound on the fp32 rounding of Lx, Ly, their squares
+// and the two sums); the box is that radius plus one pixel.
+__host__ __device__ inline void prep_sphere(const float* o, float radius, float dx, float dy,
+                                            float dz, float dw, int width, int row_begin,
+                                            int row_end, SphRec* rec, Box* box,
+                                            bool* nonfinite) {
+    *box = empty_box();
+    *nonfinite = !(std::isfinite(o[0]) && std::isfinite(o[1]) && std::isfinite(o[2]) &&
+                   std::isfinite(o[3]) && std::isfinite(radius));
+    const float lz = o[2] - 0.0f;
+    const float lw = o[3] - 1.0f;
+    const float tca = (lz * dz) + (lw * dw);  // + (Lx*dx + Ly*dy) == +-0
+    const float kzw = (lz * lz) + (lw * lw);
+    const float tca2 = tca * tca;
+    const float r2 = radius * radius;
+    rec->cx = o[0];
+    rec->cy = o[1];
+    rec->kzw = kzw;
+    rec->tca2 = tca2;
+    rec->r2 = r2;
+    rec->tca = tca;
+    rec->pad0 = rec->pad1 = 0.0f;
+    (void)dx;
+    (void)dy;
+    if (*nonfinite || !(tca >= 0.0f)) return;  // tca < 0 (or NaN): never a hit
+    const double e = 1.1920928955078125e-07;  // 2^-23
+    const double bound = ((double)r2 - ((double)kzw - (double)tca2) +
+                          8.0 * e * (fabs((double)kzw) + fabs((double)tca2))) /
+                         (1.0 - 8.0 * e);
+    if (!(bound >= 0.0)) return;  // every pixel misses
+    const double r = sqrt(bound * (1.0 + 1e-6) + 1e-6) + 1.0;
+    const double cx = o[0], cy = o[1];
+    if (cx + r < 0.0 || cx - r > (double)(width - 1) || cy + r < (double)row_begin ||
+        cy - r > (double)(row_end - 1))
+        return;
+    box->x0 = clamp_floor(cx - r, 0, width - 1);
+    box->x1 = clamp_ceil(cx + r, 0, width - 1);
+    box->y0 = clamp_floor(cy - r, row_begin, row_end - 1);
+    box->y1 = clamp_ceil(cy + r, row_begin, row_end - 1);
+}
+
+// (int)f as x86-64 cvttss2si: truncation, NaN / out of range -> INT32_MIN.
+__device__ __forceinline__ int cvt_i32(float f) {
+    return (f >= -2147483648.0f && f < 2147483648.0f) ? (int)f : INT32_MIN;
+}
+
+// MainState.cpp:396-407 + :952-955 (or the Texture packing :1026-1036).
+__device__ __forceinline__ int4v shade(float closest, float4 colour) {
+    if (closest == kFar) return int4v{0, 0, 0, 255};
+    const float normalised = (closest - 0.0f) / (180.0f - 0.0f);
+    const float scalar = 255.0f - (normalised * 255.0f);
+    return int4v{cvt_i32(scalar * colour.x), cvt_i32(scalar * colour.y),
+                 cvt_i32(scalar * colour.z), 255};
+}
+
+__device__ __forceinline__ unsigned pack_rgba8(int4v p) {
+    return (unsigned)(unsigned char)p.x | ((unsigned)(unsigned char)p.y << 8) |
+           ((unsigned)(unsigned char)p.z << 16) | 0xFF000000u;
+}
+
+// ---------------------------------------------------------------------------
+// Generic per-pixel path: the reference algorithm verbatim (any origin and
+// direction).  MainState.cpp:257-298 (fp64 MT), :300-327, :330-408.
+// ---------------------------------------------------------------------------
+__device__ inline int intersect_tri(const double* orig, const double* dir, const double* v0,
+                                    const double* v1, const double* v2, double* t) {
+    double e1[3], e2[3], tv[3], pv[3], qv[3];
+    e1[0] = v1[0] - v0[0]; e1[1] = v1[1] - v0[1]; e1[2] = v1[2] - v0[2];
+    e2[0] = v2[0] - v0[0]; e2[1] = v2[1] - v0[1]; e2[2] = v2[2] - v0[2];
+    pv[0] = dir[1] * e2[2] - dir[2] * e2[1];
+    pv[1] = dir[2] * e2[0] - dir[0] * e2[2];
+    pv[2] = dir[0] * e2[1] - dir[1] * e2[0];
+    const double det = e1[0] * pv[0] + e1[1] * pv[1] + e1[2] * pv[2];
+    if (det > -kEpsilon && det < kEpsilon) return 0;
+    const double inv_det = 1.0 / det;
+    tv[0] = orig[0] - v0[0]; tv[1] = orig[1] - v0[1]; tv[2] = orig[2] - v0[2];
+    const double u = (tv[0] * pv[0] + tv[1] * pv[1] + tv[2] * pv[2]) * inv_det;
+    if (u < 0.0 || u > 1.0) return 0;
+    qv[0] = tv[1] * e1[2] - tv[2] * e1[1];
+    qv[1] = tv[2] * e1[0] - tv[0] * e1[2];
+    qv[2] = tv[0] * e1[1] - tv[1] * e1[0];
+    const double v = (dir[0] * qv[0] + dir[1] * qv[1] + dir[2] * qv[2]) * inv_det;
+    if (v < 0.0 || u + v > 1.0) return 0;
+    *t = (e2[0] * qv[0] + e2[1] * qv[1] + e2[2] * qv[2]) * inv_det;
+    return 1;
+}
+
+__device__ inline float dot4(float4 a, float4 b) {
+    return ((a.x * b.x) + (a.y * b.y)) + ((a.z * b.z) + (a.w * b.w));
+}
+
+__device__ inline float intersect_sphere(float4 o, float4 d, float radius, float4 c) {
+    const float4 l = make_float4(c.x - o.x, c.y - o.y, c.z - o.z, c.w - o.w);
+    const float tca = dot4(l, d);
+    if (tca < 0) return 0.0f;
+    const float dist2 = dot4(l, l) - tca * tca;
+    const float r2 = radius * radius;
+    if (dist2 > r2) return 0.0f;
+    const float thc = sqrtf(r2 - dist2);
+    return tca - thc;
+}
+
+struct SceneDev {
+    const float4* __restrict__ sphere_origins;
+    const float* __restrict__ sphere_radius;
+    const float4* __restrict__ sphere_colours;
+    const float4* __restrict__ cube_vertices;
+    const float4* __restrict__ cube_colours;
+    int n_spheres, n_cubes;
+};
+
+__device__ inline int4v collide_generic(const SceneDev& s, float4 origin, float4 dir) {
+    const double o[3] = {origin.x, origin.y, origin.z};
+    const double d[3] = {dir.x, dir.y, dir.z};
+    float closest = kFar;
+    float4 colour = make_float4(0.0f, 0.0f, 0.0f, 255.0f);
+    for (int c = 0; c < s.n_cubes; ++c) {
+        const float4* tri = s.cube_vertices + 36 * c;
+        for (int k = 0; k < 36; k += 3) {
+            const float4 a = tri[k], b = tri[k + 1], e = tri[k + 2];
+            const double v0[3] = {a.x, a.y, a.z}, v1[3] = {b.x, b.y, b.z}, v2[3] = {e.x, e.y, e.z};
+            double t;
+            if (intersect_tri(o, d, v0, v1, v2, &t) == 1 && (float)t < closest) {
+                closest = (float)t;
+                colour = s.cube_colours[c];
+            }
+        }
+    }
+    for (int i = 0; i < s.n_spheres; ++i) {
+        const float dist = intersect_sphere(origin, dir, s.sphere_radius[i], s.sphere_origins[i]);
+        if (dist == 0.0f) continue;
+        if (dist < closest) {
+            closest = dist;
+            colour = s.sphere_colours[i];
+        }
+    }
+    return shade(closest, colour);
+}
+
+__global__ void __launch_bounds__(kThreads) generic_kernel(
+    SceneDev scene, float4 dir, const float4* __restrict__ origins, int width,
+    int row_begin, int row_end, int out_format, void* __restrict__ out) {
+    const int64_t n = (int64_t)width * (row_end - row_begin);
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int x = (int)(i % width);
+    const int y = row_begin + (int)(i / width);
+    const float4 o = origins ? origins[(int64_t)y * width + x]
+                             : make_float4((float)x, (float)y, 0.0f, 1.0f);
+    const int4v p = collide_generic(scene, o, dir);
+    if (out_format == RT_FORMAT_I32X4)
+        reinterpret_cast<int4v*>(out)[i] = p;
+    else
+        reinterpret_cast<unsigned*>(out)[i] = pack_rgba8(p);
+}
+
+// ---------------------------------------------------------------------------
+// Binned path
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(kThreads) prep_kernel(
+    SceneDev scene, float4 dir, int width, int row_begin, int row_end,
+    TriRec* __restrict__ tri, SphRec* __restrict__ sph, int4* __restrict__ boxes,
+    int* __restrict__ nonfinite_flag) {
+    const int n_tri = 12 * scene.n_cubes;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    Box b = empty_box();
+    bool bad = false;
+    if (i < n_tri) {
+        const float4* v = scene.cube_vertices + 3 * i;
+        const float4 a = v[0], bb = v[1], c = v[2];
+        const float fa[3] = {a.x, a.y, a.z}, fb[3] = {bb.x, bb.y, bb.z}, fc[3] = {c.x, c.y, c.z};
+        TriRec r{};
+        prep_triangle(fa, fb, fc, (double)dir.x, (double)dir.y, (double)dir.z, width, row_begin,
+                      row_end, &r, &b, &bad);
+        tri[i] = r;
+    } else if (i < n_tri + scene.n_spheres) {
+        const int s = i - n_tri;
+        const float4 o = scene.sphere_origins[s];
+        const float fo[4] = {o.x, o.y, o.z, o.w};
+        SphRec r{};
+        prep_sphere(fo, scene.sphere_radius[s], dir.x, dir.y, dir.z, dir.w, width, row_begin,
+                    row_end, &r, &b, &bad);
+        sph[s] = r;
+    } else {
+        return;
+    }
+    boxes[i] = make_int4(b.x0, b.y0, b.x1, b.y1);
+    if (bad) atomicOr(nonfinite_flag, 1);
+}
+
+// masks[w * n_bins + bin] bit j = primitive 64 w + j may touch bin `bin`.
+__global__ void __launch_bounds__(kThreads) bin_kernel(
+    const int4* __restrict__ boxes, int n_prims, int n_bins_x, int n_bins, int row_begin,
+    int n_words, unsigned long long* __restrict__ masks) {
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= (int64_t)n_words * n_bins) return;
+    const int w = (int)(gid / n_bins);
+    const int bin = (int)(gid % n_bins);
+    const int x0 = (bin % n_bins_x) * kBinW, x1 = x0 + kBinW - 1;
+    const int y0 = row_begin + (bin / n_bins_x) * kBinH, y1 = y0 + kBinH - 1;
+    unsigned long long m = 0;
+    const int base = w * 64;
+    const int lim = min(64, n_prims - base);
+    for (int j = 0; j < lim; ++j) {
+        const int4 b = boxes[base + j];
+        const bool hit = b.x <= x1 && b.z >= x0 && b.y <= y1 && b.w >= y0;
+        m |= (unsigned long long)hit << j;
+    }
+    masks[gid] = m;
+}
+
+__global__ void __launch_bounds__(kThreads) trace_kernel(
+    SceneDev scene, const TriRec* __restrict__ tri, const SphRec* __restrict__ sph,
+    const int4* __restrict__ boxes, const unsigned long long* __restrict__ masks,
+    const int* __restrict__ nonfinite_flag, float4 dir, int width, int row_begin,
+    int row_end, int n_bins_x, int n_bins, int n_words, int out_format,
+    void* __restrict__ out) {
+    const int bin = blockIdx.x;
+    const int wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int tile_x = (bin % n_bins_x) * kBinW + (wave & 1) * kWaveTile;
+    const int tile_y = row_begin + (bin / n_bins_x) * kBinH + (wave >> 1) * kWaveTile;
+    const int x = tile_x + (lane & 15);
+    const int y0 = tile_y + (lane >> 4);
+    const int n_tri = 12 * scene.n_cubes;
+
+    float closest[kRowsPerLane];
+    int hit[kRowsPerLane];
+#pragma unroll
+    for (int j = 0; j < kRowsPerLane; ++j) {
+        closest[j] = kFar;
+        hit[j] = -1;
+    }
+
+    if (*nonfinite_flag) {
+        // Non-finite scene data: the algebraic shortcuts of the binned path
+        // assume finite values, so run the reference algorithm verbatim.
+#pragma unroll 1
+        for (int j = 0; j < kRowsPerLane; ++j) {
+            const int y = y0 + 4 * j;
+            if (x >= width || y >= row_end) continue;
+            const int4v p =
+                collide_generic(scene, make_float4((float)x, (float)y, 0.0f, 1.0f), dir);
+            const int64_t idx = (int64_t)(y - row_begin) * width + x;
+            if (out_format == RT_FORMAT_I32X4)
+                reinterpret_cast<int4v*>(out)[idx] = p;
+            else
+                reinterpret_cast<unsigned*>(out)[idx] = pack_rgba8(p);
+        }
+        return;
+    }
+
+    const double px = (double)x;
+    const float pxf = (float)x;
+    double py[kRowsPerLane];
+    float pyf[kRowsPerLane];
+#pragma unroll
+    for (int j = 0; j < kRowsPerLane; ++j) {
+        py[j] = (double)(y0 + 4 * j);
+        pyf[j] = (float)(y0 + 4 * j);
+    }
+    const int tx1 = tile_x + kWaveTile - 1, ty1 = tile_y + kWaveTile - 1;
+
+    for (int w = 0; w < n_words; ++w) {
+        unsigned long long m = masks[(int64_t)w * n_bins + bin];
+        while (m) {
+            const int p = w * 64 + __builtin_ctzll(m);
+            m &= m - 1;
+            const int4 b = boxes[p];
+            if (b.x > tx1 || b.z < tile_x || b.y > ty1 || b.w < tile_y) continue;
+            if (p < n_tri) {
+                const TriRec r = tri[p];
+                const double tx = px - r.v0x;
+#pragma unroll
+                for (int j = 0; j < kRowsPerLane; ++j) {
+                    const double ty = py[j] - r.v0y;
+                    // u = ((tx*p0 + ty*p1) + tz*p2) * inv_det with tz*p2 == +-0
+                    const double u = (tx * r.p0 + ty * r.p1) * r.inv_det;
+                    // v = ((d0*q0 + d1*q1) + d2*q2) * inv_det with d0 = d1 = +-0
+                    const double q2 = tx * r.e1y - ty * r.e1x;
+                    const double v = (r.dz * q2) * r.inv_det;
+                    const bool inside = !(u < 0.0 || u > 1.0) && !(v < 0.0 || u + v > 1.0);
+                    if (inside) {
+                        const double q0 = ty * r.e1z - r.k0;
+                        const double q1 = r.k1 - tx * r.e1z;
+                        const double t = (r.e2x * q0 + r.e2y * q1 + r.e2z * q2) * r.inv_det;
+                        const float tf = (float)t;
+                        if (tf < closest[j]) {
+                            closest[j] = tf;
+                            hit[j] = p;
+                        }
+                    }
+                }
+            } else {
+                const SphRec s = sph[p - n_tri];
+                const float lx = s.cx - pxf;
+                const float lx2 = lx * lx;
+#pragma unroll
+                for (int j = 0; j < kRowsPerLane; ++j) {
+                    const float ly = s.cy - pyf[j];
+                    const float a = lx2 + ly * ly;
+                    const float dist2 = (a + s.kzw) - s.tca2;
+                    if (!(dist2 > s.r2)) {
+                        const float thc = sqrtf(s.r2 - dist2);
+                        const float t0 = s.tca - thc;
+                        if (t0 != 0.0f && t0 < closest[j]) {
+                            closest[j] = t0;
+                            hit[j] = p;
+                        }
+                    }
+                }
+            }
+        }
+    }
+
+    // Shade + store.  Waves with no hit at all store the black pattern
+    // without touching the colour arrays.
+    const bool any_hit =
+        __ballot(hit[0] >= 0 || hit[1] >= 0 || hit[2] >= 0 || hit[3] >= 0) != 0ull;
+#pragma unroll
+    for (int j = 0; j < kRowsPerLane; ++j) {
+        const int y = y0 + 4 * j;
+        int4v pix{0, 0, 0, 255};
+        if (any_hit && hit[j] >= 0) {
+            const float4 col = hit[j] < n_tri ? scene.cube_colours[hit[j] / 12]
+                                              : scene.sphere_colours[hit[j] - n_tri];
+            pix = shade(closest[j], col);
+        }
+        if (x < width && y < row_end) {
+            const int64_t idx = (int64_t)(y - row_begin) * width + x;
+            if (out_format == RT_FORMAT_I32X4)
+                reinterpret_cast<int4v*>(out)[idx] = pix;
+            else
+                reinterpret_cast<unsigned*>(out)[idx] = pack_rgba8(pix);
+        }
+    }
+}
+
+// fp32 self-test: the device's sqrtf and '/' must be correctly rounded.
+__global__ void fp32_selftest_kernel(const float* in, int n, float* out_sqrt, float* out_div) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    out_sqrt[i] = sqrtf(in[i]);
+    out_div[i] = in[i] / 180.0f;
+}
+
+}  // namespace
+
+// ===========================================================================
+// Host side
+// ===========================================================================
+struct rt_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    // workspace (grow-only)
+    void* scene_buf = nullptr;  size_t scene_cap = 0;   // host-API scene copy
+    void* origin_buf = nullptr; size_t origin_cap = 0;  // host-API explicit origins
+    void* out_buf = nullptr;    size_t out_cap = 0;     // host-API frame
+    void* rec_buf = nullptr;    size_t rec_cap = 0;     // TriRec/SphRec/boxes/flag
+    void* mask_buf = nullptr;   size_t mask_cap = 0;    // bin masks
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    // profiling
+    bool profile = false;
+    std::vector<hipEvent_t> prof_events;  // quads: start, prep, bin, trace
+    int32_t prof_count = 0;
+};
+
+namespace {
+
+size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+int ensure(void** buf, size_t* cap, size_t need) {
+    if (need <= *cap) return RT_OK;
+    if (*buf) {
+        (void)hipFree(*buf);
+        *buf = nullptr;
+        *cap = 0;
+    }
+    size_t n = align_up(need + need / 4, 1 << 16);
+    if (hipMalloc(buf, n) != hipSuccess) {
+        *buf = nullptr;
+        return RT_ERR_OUT_OF_MEMORY;
+    }
+    *cap = n;
+    return RT_OK;
+}
+
+bool binned_ok(const float d[4], const float* origins) {
+    return origins == nullptr && d[0] == 0.0f && d[1] == 0.0f && d[2] != 0.0f &&
+           std::isfinite(d[2]) && std::isfinite(d[3]);
+}
+
+int check_args(const rt_scene* s, int32_t width, int32_t height, int32_t row_begin,
+               int32_t row_end, int32_t fmt) {
+    if (!s || width <= 0 || height <= 0 || row_begin < 0 || row_end > height ||
+        row_begin >= row_end)
+        return RT_ERR_INVALID_ARG;
+    if (width > (1 << 24) || height > (1 << 24)) return RT_ERR_INVALID_ARG;  // exact float coords
+    if (s->num_spheres < 0 || s->num_cubes < 0 || s->num_lights < 0) return RT_ERR_INVALID_ARG;
+    if (s->num_spheres > 0 && (!s->sphere_origins || !s->sphere_radius || !s->sphere_colours))
+        return RT_ERR_INVALID_ARG;
+    if (s->num_cubes > 0 && (!s->cube_vertices || !s->cube_colours)) return RT_ERR_INVALID_ARG;
+    if ((int64_t)12 * s->num_cubes + s->num_spheres > (int64_t)1 << 30) return RT_ERR_INVALID_ARG;
+    if (fmt != RT_FORMAT_I32X4 && fmt != RT_FORMAT_RGBA8) return RT_ERR_INVALID_ARG;
+    return RT_OK;
+}
+
+#define HIP_TRY(x)                                    \
+    do {                                              \
+        if ((x) != hipSuccess) return RT_ERR_HIP;     \
+    } while (0)
+
+// Enqueue one render of rows [row_begin, row_end) on `stream`.  All scene
+// pointers are device pointers.
+int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origins,
+           int32_t width, int32_t row_begin, int32_t row_end, int32_t fmt, int32_t path,
+           void* out, hipStream_t stream, int32_t* used_path) {
+    SceneDev sd{reinterpret_cast<const float4*>(s->sphere_origins), s->sphere_radius,
+                reinterpret_cast<const float4*>(s->sphere_colours),
+                reinterpret_cast<const float4*>(s->cube_vertices),
+                reinterpret_cast<const float4*>(s->cube_colours), s->num_spheres, s->num_cubes};
+    const float4 dir = make_float4(d[0], d[1], d[2], d[3]);
+    const int32_t rows = row_end - row_begin;
+    const bool can_bin = binned_ok(d, origins);
+    if (path == RT_PATH_BINNED && !can_bin) return RT_ERR_UNSUPPORTED;
+    const bool use_bin = path == RT_PATH_BINNED || (path == RT_PATH_AUTO && can_bin);
+    if (used_path) *used_path = use_bin ? RT_PATH_BINNED : RT_PATH_GENERIC;
+    hipEvent_t* pe = nullptr;
+    if (ctx->profile) {
+        for (int k = 0; k < 4; ++k) {
+            hipEvent_t e;
+            HIP_TRY(hipEventCreate(&e));
+            ctx->prof_events.push_back(e);
+        }
+        pe = &ctx->prof_events[ctx->prof_events.size() - 4];
+        HIP_TRY(hipEventRecord(pe[0], stream));
+        ++ctx->prof_count;
+    }
+    if (!use_bin) {
+        const int64_t n = (int64_t)width * rows;
+        const int64_t blocks = (n + kThreads - 1) / kThreads;
+        if (pe) {
+            HIP_TRY(hipEventRecord(pe[1], stream));
+            HIP_TRY(hipEventRecord(pe[2], stream));
+        }
+        generic_kernel<<<dim3((unsigned)blocks), dim3(kThreads), 0, stream>>>(
+            sd, dir, reinterpret_cast<const float4*>(origins), width, row_begin, row_end, fmt,
+            out);
+        HIP_TRY(hipGetLastError());
+        if (pe) HIP_TRY(hipEventRecord(pe[3], stream));
+        return RT_OK;
+    }
+    const int n_tri = 12 * s->num_cubes;
+    const int n_prims = n_tri + s->num_spheres;
+    const int n_words = (n_prims + 63) / 64;
+    const int n_bins_x = (width + kBinW - 1) / kBinW;
+    const int n_bins_y = (rows + kBinH - 1) / kBinH;
+    const int64_t n_bins64 = (int64_t)n_bins_x * n_bins_y;
+    if (n_bins64 > (int64_t)1 << 31) return RT_ERR_INVALID_ARG;
+    const int n_bins = (int)n_bins64;
+
+    const size_t tri_off = 0;
+    const size_t sph_off = align_up(sizeof(TriRec) * (size_t)n_tri, 256);
+    const size_t box_off = sph_off + align_up(sizeof(SphRec) * (size_t)s->num_spheres, 256);
+    const size_t flag_off = box_off + align_up(sizeof(int4) * (size_t)n_prims, 256);
+    const size_t rec_need = flag_off + 256;
+    int rc = ensure(&ctx->rec_buf, &ctx->rec_cap, rec_need);
+    if (rc) return rc;
+    const size_t mask_need = sizeof(unsigned long long) * (size_t)n_words * (size_t)n_bins + 256;
+    rc = ensure(&ctx->mask_buf, &ctx->mask_cap, mask_need);
+    if (rc) return rc;
+    char* base = static_cast<char*>(ctx->rec_buf);
+    TriRec* tri = reinterpret_cast<TriRec*>(base + tri_off);
+    SphRec* sph = reinterpret_cast<SphRec*>(base + sph_off);
+    int4* boxes = reinterpret_cast<int4*>(base + box_off);
+    int* flag = reinterpret_cast<int*>(base + flag_off);
+    auto* masks = static_cast<unsigned long long*>(ctx->mask_buf);
+
+    HIP_TRY(hipMemsetAsync(flag, 0, sizeof(int), stream));
+    if (n_prims > 0) {
+        prep_kernel<<<dim3((n_prims + kThreads - 1) / kThreads), dim3(kThreads), 0, stream>>>(
+            sd, dir, width, row_begin, row_end, tri, sph, boxes, flag);
+        HIP_TRY(hipGetLastError());
+    }
+    if (pe) HIP_TRY(hipEventRecord(pe[1], stream));
+    if (n_words > 0) {
+        const int64_t n = (int64_t)n_words * n_bins;
+        bin_kernel<<<dim3((unsigned)((n + kThreads - 1) / kThreads)), dim3(kThreads), 0,
+                     stream>>>(boxes, n_prims, n_bins_x, n_bins, row_begin, n_words, masks);
+        HIP_TRY(hipGetLastError());
+    }
+    if (pe) HIP_TRY(hipEventRecord(pe[2], stream));
+    trace_kernel<<<dim3((unsigned)n_bins), dim3(kThreads), 0, stream>>>(
+        sd, tri, sph, boxes, masks, flag, dir, width, row_begin, row_end, n_bins_x, n_bins,
+        n_words, fmt, out);
+    HIP_TRY(hipGetLastError());
+    if (pe) HIP_TRY(hipEventRecord(pe[3], stream));
+    return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* rt_error_string(int status) {
+    switch (status) {
+    case RT_OK: return "success";
+    case RT_ERR_INVALID_ARG: return "invalid argument";
+    case RT_ERR_NO_DEVICE: return "no HIP device available";
+    case RT_ERR_HIP: return "HIP runtime error";
+    case RT_ERR_OUT_OF_MEMORY: return "device out of memory";
+    case RT_ERR_UNSUPPORTED: return "requested path unsupported for these rays";
+    default: return "unknown error";
+    }
+}
+
+int rt_init(int device_ordinal, rt_ctx** out_ctx) {
+    if (!out_ctx) return RT_ERR_INVALID_ARG;
+    *out_ctx = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return RT_ERR_NO_DEVICE;
+    if (device_ordinal < 0 || device_ordinal >= n) return RT_ERR_INVALID_ARG;
+    if (hipSetDevice(device_ordinal) != hipSuccess) return RT_ERR_HIP;
+    rt_ctx* ctx = new rt_ctx();
+    ctx->device = device_ordinal;
+    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete ctx;
+        return RT_ERR_HIP;
+    }
+    for (auto& e : ctx->ev) {
+        if (hipEventCreate(&e) != hipSuccess) {
+            rt_destroy(ctx);
+            return RT_ERR_HIP;
+        }
+    }
+    *out_ctx = ctx;
+    return RT_OK;
+}
+
+void rt_destroy(rt_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    for (void* p : {ctx->scene_buf, ctx->origin_buf, ctx->out_buf, ctx->rec_buf, ctx->mask_buf})
+        if (p) (void)hipFree(p);
+    for (auto& e : ctx->ev)
+        if (e) (void)hipEventDestroy(e);
+    for (auto e : ctx->prof_events) (void)hipEventDestroy(e);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+int rt_render_path(rt_ctx* ctx, const rt_scene* scene, const float ray_dir[4],
+                   const float* ray_origins, int32_t width, int32_t height, int32_t row_begin,
+                   int32_t row_end, int32_t out_format, int32_t path, void* host_out,
+                   rt_timing* timing) {
+    const auto t0 = std::chrono::steady_clock::now();
+    if (!ctx || !ray_dir || !host_out) return RT_ERR_INVALID_ARG;
+    int rc = check_args(scene, width, height, row_begin, row_end, out_format);
+    if (rc) return rc;
+    if (path < RT_PATH_AUTO || path > RT_PATH_GENERIC) return RT_ERR_INVALID_ARG;
+    HIP_TRY(hipSetDevice(ctx->device));
+    const int32_t rows = row_end - row_begin;
+    const size_t ns = (size_t)scene->num_spheres, nc = (size_t)scene->num_cubes;
+    // one device copy of the flattened scene (MainState.cpp:666-743, 759-838)
+    const size_t o_so = 0, o_sr = align_up(16 * ns, 256), o_sc = o_sr + align_up(4 * ns, 256),
+                 o_cv = o_sc + align_up(16 * ns, 256), o_cc = o_cv + align_up(16 * 36 * nc, 256),
+                 scene_bytes = o_cc + align_up(16 * nc, 256) + 256;
+    rc = ensure(&ctx->scene_buf, &ctx->scene_cap, scene_bytes);
+    if (rc) return rc;
+    const size_t px = (size_t)width * rows;
+    const size_t out_bytes = px * (out_format == RT_FORMAT_I32X4 ? 16 : 4);
+    rc = ensure(&ctx->out_buf, &ctx->out_cap, out_bytes);
+    if (rc) return rc;
+    char* sb = static_cast<char*>(ctx->scene_buf);
+    hipStream_t st = ctx->stream;
+    HIP_TRY(hipEventRecord(ctx->ev[0], st));
+    if (ns) {
+        HIP_TRY(hipMemcpyAsync(sb + o_so, scene->sphere_origins, 16 * ns, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(sb + o_sr, scene->sphere_radius, 4 * ns, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(sb + o_sc, scene->sphere_colours, 16 * ns, hipMemcpyHostToDevice, st));
+    }
+    if (nc) {
+        HIP_TRY(hipMemcpyAsync(sb + o_cv, scene->cube_vertices, 16 * 36 * nc, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(sb + o_cc, scene->cube_colours, 16 * nc, hipMemcpyHostToDevice, st));
+    }
+    const float* d_origins = nullptr;
+    if (ray_origins) {  // the reference uploads all W*H origins (MainState.cpp:841-855)
+        const size_t ob = (size_t)width * height * 16;
+        rc = ensure(&ctx->origin_buf, &ctx->origin_cap, ob);
+        if (rc) return rc;
+        HIP_TRY(hipMemcpyAsync(ctx->origin_buf, ray_origins, ob, hipMemcpyHostToDevice, st));
+        d_origins = static_cast<const float*>(ctx->origin_buf);
+    }
+    rt_scene dscene = *scene;
+    dscene.sphere_origins = reinterpret_cast<const float*>(sb + o_so);
+    dscene.sphere_radius = reinterpret_cast<const float*>(sb + o_sr);
+    dscene.sphere_colours = reinterpret_cast<const float*>(sb + o_sc);
+    dscene.cube_vertices = reinterpret_cast<const float*>(sb + o_cv);
+    dscene.cube_colours = reinterpret_cast<const float*>(sb + o_cc);
+    HIP_TRY(hipEventRecord(ctx->ev[1], st));
+    int32_t used = 0;
+    rc = launch(ctx, &dscene, ray_dir, d_origins, width, row_begin, row_end, out_format, path,
+                ctx->out_buf, st, &used);
+    if (rc) return rc;
+    HIP_TRY(hipEventRecord(ctx->ev[2], st));
+    HIP_TRY(hipMemcpyAsync(host_out, ctx->out_buf, out_bytes, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipEventRecord(ctx->ev[3], st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (timing) {
+        float a = 0, b = 0, c = 0;
+        (void)hipEventElapsedTime(&a, ctx->ev[0], ctx->ev[1]);
+        (void)hipEventElapsedTime(&b, ctx->ev[1], ctx->ev[2]);
+        (void)hipEventElapsedTime(&c, ctx->ev[2], ctx->ev[3]);
+        timing->upload_us = 1e3 * a;
+        timing->kernel_us = 1e3 * b;
+        timing->download_us = 1e3 * c;
+        timing->path = used;
+        timing->total_us = std::chrono::duration<double, std::micro>(
+                               std::chrono::steady_clock::now() - t0).count();
+    }
+    return RT_OK;
+}
+
+int rt_render(rt_ctx* ctx, const rt_scene* scene, const float ray_dir[4], const float* ray_origins,
+              int32_t width, int32_t height, int32_t row_begin, int32_t row_end,
+              int32_t out_format, void* host_out, rt_timing* timing) {
+    return rt_render_path(ctx, scene, ray_dir, ray_origins, width, height, row_begin, row_end,
+                          out_format, RT_PATH_AUTO, host_out, timing);
+}
+
+int rt_render_device(rt_ctx* ctx, const rt_scene* device_scene, const float ray_dir[4],
+                     const float* device_ray_origins, int32_t width, int32_t height,
+                     int32_t row_begin, int32_t row_end, int32_t out_format, int32_t path,
+                     void* device_out, void* stream) {
+    if (!ctx || !ray_dir || !device_out) return RT_ERR_INVALID_ARG;
+    int rc = check_args(device_scene, width, height, row_begin, row_end, out_format);
+    if (rc) return rc;
+    if (path < RT_PATH_AUTO || path > RT_PATH_GENERIC) return RT_ERR_INVALID_ARG;
+    HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    return launch(ctx, device_scene, ray_dir, device_ray_origins, width, row_begin, row_end,
+                  out_format, path, device_out, st, nullptr);
+}
+
+int rt_profile_enable(rt_ctx* ctx, int enable) {
+    if (!ctx) return RT_ERR_INVALID_ARG;
+    ctx->profile = enable != 0;
+    return RT_OK;
+}
+
+int rt_profile_read(rt_ctx* ctx, double* prep_ms, double* bin_ms, double* trace_ms,
+                    int32_t* n_renders) {
+    if (!ctx) return RT_ERR_INVALID_ARG;
+    HIP_TRY(hipSetDevice(ctx->device));
+    double sums[3] = {0, 0, 0};
+    for (size_t q = 0; q + 3 < ctx->prof_events.size(); q += 4) {
+        HIP_TRY(hipEventSynchronize(ctx->prof_events[q + 3]));
+        for (int k = 0; k < 3; ++k) {
+            float ms = 0.0f;
+            HIP_TRY(hipEventElapsedTime(&ms, ctx->prof_events[q + k], ctx->prof_events[q + k + 1]));
+            sums[k] += ms;
+        }
+    }
+    if (prep_ms) *prep_ms = sums[0];
+    if (bin_ms) *bin_ms = sums[1];
+    if (trace_ms) *trace_ms = sums[2];
+    if (n_renders) *n_renders = ctx->prof_count;
+    for (auto e : ctx->prof_events) (void)hipEventDestroy(e);
+    ctx->prof_events.clear();
+    ctx->prof_count = 0;
+    return RT_OK;
+}
+
+int rt_device_info(rt_ctx* ctx, char* name, int32_t name_len, int32_t* n_cu, int64_t* total_mem) {
+    if (!ctx) return RT_ERR_INVALID_ARG;
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, ctx->device));
+    if (name && name_len > 0) {
+        std::snprintf(name, (size_t)name_len, "%s (%s)", prop.name, prop.gcnArchName);
+    }
+    if (n_cu) *n_cu = prop.multiProcessorCount;
+    if (total_mem) *total_mem = (int64_t)prop.totalGlobalMem;
+    return RT_OK;
+}
+
+// Test hooks (not part of the reference interface).
+int rt_selftest_fp32(rt_ctx* ctx, const float* host_in, int32_t n, float* host_sqrt,
+                     float* host_div) {
+    if (!ctx || !host_in || n <= 0 || !host_sqrt || !host_div) return RT_ERR_INVALID_ARG;
+    HIP_TRY(hipSetDevice(ctx->device));
+    float* d = nullptr;
+    HIP_TRY(hipMalloc(&d, sizeof(float) * 3 * (size_t)n));
+    HIP_TRY(hipMemcpy(d, host_in, sizeof(float) * n, hipMemcpyHostToDevice));
+    fp32_selftest_kernel<<<dim3((n + 255) / 256), dim3(256), 0, ctx->stream>>>(d, n, d + n,
+                                                                            d + 2 * (size_t)n);
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    HIP_TRY(hipMemcpy(host_sqrt, d + n, sizeof(float) * n, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(host_div, d + 2 * (size_t)n, sizeof(float) * n, hipMemcpyDeviceToHost));
+    (void)hipFree(d);
+    return RT_OK;
+}
+
+// Host evaluation of the prep step (same __host__ __device__ code the prep
+// kernel runs), for the CPU-side culling-bound tests.  Writes the box as
+// int32[4] (x0, y0, x1, y1) and returns 1 when the triangle is valid.
+int rt_debug_triangle_box(const float v0[3], const float v1[3], const float v2[3],
+                          const float dir[4], int32_t width, int32_t row_begin, int32_t row_end,
+                          int32_t box_out[4]) {
+    TriRec r{};
+    Box b{};
+    bool bad = false;
+    const bool ok = prep_triangle(v0, v1, v2, dir[0], dir[1], dir[2], width, row_begin, row_end,
+                                  &r, &b, &bad);
+    box_out[0] = b.x0; box_out[1] = b.y0; box_out[2] = b.x1; box_out[3] = b.y1;
+    return ok ? 1 : 0;
+}
+
+int rt_debug_sphere_box(const float origin[4], float radius, const float dir[4], int32_t width,
+                        int32_t row_begin, int32_t row_end, int32_t box_out[4]) {
+    SphRec r{};
+    Box b{};
+    bool bad = false;
+    prep_sphere(origin, radius, dir[0], dir[1], dir[2], dir[3], width, row_begin, row_end, &r, &b,
+                &bad);
+    box_out[0] = b.x0; box_out[1] = b.y0; box_out[2] = b.x1; box_out[3] = b.y1;
+    return bad ? 0 : 1;
+}
+
+}  // extern "C"

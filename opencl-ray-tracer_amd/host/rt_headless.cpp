@@ -1,0 +1,136 @@
+// rt_headless.cpp -- headless C++ host for librt_hip.so.
+//
+// Stands where the reference's MainState sits (RayTrace/states/MainState.cpp):
+// it builds a scene (createScene1/2/3, :419-639, or the synthetic benchmark
+// scene), traces it through the C ABI exactly as the rewritten
+// MainState::executeRayTracerOpenCL would, prints the
+// reference's timing line (:903) and an FNV-1a-64 hash of the int32 frame,
+// and can dump the Texture conversion (:974-1045) as a PPM image.
+//
+//   rt_headless [--scene 1|2|3] [--seed S] [--width W] [--height H]
+//               [--synthetic N M k] [--rows A B] [--ppm out.ppm] [--repeat R]
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "rt_hip.h"
+
+namespace {
+
+uint64_t fnv1a(const int32_t* v, size_t n) {
+    uint64_t h = 0xcbf29ce484222325ull;
+    for (size_t i = 0; i < n; ++i) {
+        h ^= static_cast<uint32_t>(v[i]);
+        h *= 0x100000001b3ull;
+    }
+    return h;
+}
+
+bool write_ppm(const std::string& path, const std::vector<int32_t>& frame, int w, int h) {
+    FILE* f = std::fopen(path.c_str(), "wb");
+    if (!f) return false;
+    std::fprintf(f, "P6\n%d %d\n255\n", w, h);
+    std::vector<unsigned char> row(3 * (size_t)w);
+    for (int y = 0; y < h; ++y) {
+        for (int x = 0; x < w; ++x)
+            for (int c = 0; c < 3; ++c)  // (uint8_t) wrap, MainState.cpp:1026-1028
+                row[3 * x + c] = static_cast<unsigned char>(frame[4 * ((size_t)y * w + x) + c]);
+        std::fwrite(row.data(), 1, row.size(), f);
+    }
+    std::fclose(f);
+    return true;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    int scene_id = 1, width = 640, height = 480, repeat = 1;
+    unsigned seed = 1;
+    int syn_n = -1, syn_m = -1;
+    float syn_k = 1.0f;
+    int row_begin = 0, row_end = -1;
+    std::string ppm;
+    for (int i = 1; i < argc; ++i) {
+        std::string a = argv[i];
+        auto next = [&](void) -> const char* {
+            if (i + 1 >= argc) {
+                std::fprintf(stderr, "missing value for %s\n", a.c_str());
+                std::exit(2);
+            }
+            return argv[++i];
+        };
+        if (a == "--scene") scene_id = std::atoi(next());
+        else if (a == "--seed") seed = (unsigned)std::strtoul(next(), nullptr, 10);
+        else if (a == "--width") width = std::atoi(next());
+        else if (a == "--height") height = std::atoi(next());
+        else if (a == "--synthetic") {
+            syn_n = std::atoi(next());
+            syn_m = std::atoi(next());
+            syn_k = (float)std::atof(next());
+        } else if (a == "--rows") {
+            row_begin = std::atoi(next());
+            row_end = std::atoi(next());
+        } else if (a == "--ppm") ppm = next();
+        else if (a == "--repeat") repeat = std::atoi(next());
+        else {
+            std::fprintf(stderr, "unknown option %s\n", a.c_str());
+            return 2;
+        }
+    }
+    if (row_end < 0) row_end = height;
+
+    // Scene vectors, MainState.h:99-106 (cubes already flattened, :646-655).
+    const int cap_s = syn_n >= 0 ? syn_n : 100, cap_c = syn_m >= 0 ? syn_m : 100;
+    std::vector<float> so(4 * (size_t)cap_s), sr((size_t)cap_s), sc(4 * (size_t)cap_s);
+    std::vector<float> cv(144 * (size_t)cap_c), cc(4 * (size_t)cap_c);
+    int32_t ns = 0, nc = 0;
+    int rc;
+    if (syn_n >= 0) {
+        rc = rt_scene_synthetic(width, height, syn_n, syn_m, seed, syn_k, so.data(), sr.data(),
+                                sc.data(), cv.data(), cc.data());
+        ns = syn_n;
+        nc = syn_m;
+    } else {
+        rc = rt_scene_reference(scene_id, seed, so.data(), sr.data(), sc.data(), cv.data(),
+                                cc.data(), &ns, &nc);
+    }
+    if (rc != RT_OK) {
+        std::fprintf(stderr, "scene construction failed: %s\n", rt_error_string(rc));
+        return 1;
+    }
+
+    rt_ctx* ctx = nullptr;  // MainState ctor -> openCLInit (:52)
+    rc = rt_init(0, &ctx);
+    if (rc != RT_OK) {
+        std::fprintf(stderr, "rt_init failed: %s\n", rt_error_string(rc));
+        return 1;
+    }
+    float ray_dir[4];
+    rt_primary_ray_dir(ray_dir);  // (0,0,-1,-1), MainState.cpp:37-39
+    rt_scene scene{so.data(), sr.data(), sc.data(), ns, cv.data(), cc.data(), nc, nullptr, 0};
+    std::vector<int32_t> pixels(4 * (size_t)width * (row_end - row_begin));
+    rt_timing t{};
+    for (int r = 0; r < repeat; ++r) {
+        std::printf("HIP Ray Tracer Begin\n");
+        rc = rt_render(ctx, &scene, ray_dir, nullptr, width, height, row_begin, row_end,
+                       RT_FORMAT_I32X4, pixels.data(), &t);
+        if (rc != RT_OK) {
+            std::fprintf(stderr, "rt_render failed: %s\n", rt_error_string(rc));
+            rt_destroy(ctx);
+            return 1;
+        }
+        std::printf("Time Taken: %.0f microseconds (upload %.1f, kernels %.1f, readback %.1f; %s path)\n",
+                    t.total_us, t.upload_us, t.kernel_us, t.download_us,
+                    t.path == RT_PATH_BINNED ? "binned" : "generic");
+    }
+    std::printf("frame %dx%d rows [%d,%d) spheres %d cubes %d fnv1a64 %016llx\n", width, height,
+                row_begin, row_end, ns, nc,
+                (unsigned long long)fnv1a(pixels.data(), pixels.size()));
+    if (!ppm.empty() && !write_ppm(ppm, pixels, width, row_end - row_begin))
+        std::fprintf(stderr, "could not write %s\n", ppm.c_str());
+    rt_destroy(ctx);
+    return 0;
+}

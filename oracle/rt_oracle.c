@@ -1,0 +1,667 @@
+/*
+ * rt_oracle.c -- TEST INFRASTRUCTURE ONLY (the checker, never the product).
+ *
+ * A plain-C restatement of the reference's serial CPU ray tracer and of the
+ * scene construction it traces.  Every function cites the reference line it
+ * follows (paths relative to /root/reference/RayTrace).  Build flags matter
+ * (SURVEY.md F6): this file is compiled with `-O2 -ffp-contract=off` for
+ * baseline x86-64 (no FMA), so every float/double operation rounds exactly
+ * once, in the reference's source order.
+ *
+ * Parity pinning (see DESIGN.md "Oracle"; checked by tests/test_oracle.py):
+ *   - frames: the statistics SURVEY.md §0/§8c recorded from the reference's
+ *     own executeRayTracerCPU, compiled and run in the survey's probe, on
+ *     scenes 1-3 at 640x480 (lit-pixel count, max channel, pixels > 255,
+ *     and the per-scene count / max size of the CPU-vs-OpenCL-kernel pixel
+ *     differences: 33/205, 33, 0).  The survey's FNV hash strings do not
+ *     reproduce under the hash definition it states; its hashing code was
+ *     not recorded, so those strings are not used as a pin;
+ *   - cube packing: the reference's own Cube.cpp, compiled unmodified from
+ *     /root/reference into oracle/_ref/libref_cube.so (oracle/Makefile),
+ *     is compared vertex-for-vertex with orc_cube_* below.
+ */
+#include "rt_oracle.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------------
+ * glm 0.9.6.1 restated (column-major, m[col][row]).
+ * ---------------------------------------------------------------------- */
+typedef struct { float c[4][4]; } mat4;
+
+static mat4 mat_identity(void) {
+    mat4 m;
+    memset(&m, 0, sizeof m);
+    m.c[0][0] = m.c[1][1] = m.c[2][2] = m.c[3][3] = 1.0f;
+    return m;
+}
+
+/* glm/detail/type_mat4x4.inl:596-607: (m0*v0 + m1*v1) + (m2*v2 + m3*v3) */
+static void mat_mul_vec(const mat4* m, const float v[4], float out[4]) {
+    for (int i = 0; i < 4; ++i) {
+        float mul0 = m->c[0][i] * v[0];
+        float mul1 = m->c[1][i] * v[1];
+        float add0 = mul0 + mul1;
+        float mul2 = m->c[2][i] * v[2];
+        float mul3 = m->c[3][i] * v[3];
+        float add1 = mul2 + mul3;
+        out[i] = add0 + add1;
+    }
+}
+
+/* glm/gtc/matrix_transform.inl:52-85 (rotate), normalize via
+ * func_geometric.inl:154-159 (x * inversesqrt(dot(x,x))), vec3 dot is
+ * (x+y)+z (func_geometric.inl:64-71), inversesqrt = 1/sqrt
+ * (func_exponential.inl:62-67). */
+static mat4 glm_rotate(const mat4* m, float angle, float ax, float ay, float az) {
+    const float a = angle;
+    const float c = cosf(a);
+    const float s = sinf(a);
+    float d = ax * ax + ay * ay + az * az;
+    float inv = 1.0f / sqrtf(d);
+    float axis[3] = {ax * inv, ay * inv, az * inv};
+    float one_c = 1.0f - c;
+    float temp[3] = {one_c * axis[0], one_c * axis[1], one_c * axis[2]};
+    float R[3][3];
+    R[0][0] = c + temp[0] * axis[0];
+    R[0][1] = 0.0f + temp[0] * axis[1] + s * axis[2];
+    R[0][2] = 0.0f + temp[0] * axis[2] - s * axis[1];
+    R[1][0] = 0.0f + temp[1] * axis[0] - s * axis[2];
+    R[1][1] = c + temp[1] * axis[1];
+    R[1][2] = 0.0f + temp[1] * axis[2] + s * axis[0];
+    R[2][0] = 0.0f + temp[2] * axis[0] + s * axis[1];
+    R[2][1] = 0.0f + temp[2] * axis[1] - s * axis[0];
+    R[2][2] = c + temp[2] * axis[2];
+    mat4 out;
+    for (int i = 0; i < 3; ++i)
+        for (int r = 0; r < 4; ++r)
+            out.c[i][r] = m->c[0][r] * R[i][0] + m->c[1][r] * R[i][1] + m->c[2][r] * R[i][2];
+    for (int r = 0; r < 4; ++r) out.c[3][r] = m->c[3][r];
+    return out;
+}
+
+/* ------------------------------------------------------------------------
+ * Cube, Cube.cpp:6-83
+ * ---------------------------------------------------------------------- */
+static const signed char kUnitCube[36][3] = { /* Cube.cpp:10-45 */
+    {-1,-1,-1},{-1,-1, 1},{-1, 1, 1}, { 1, 1,-1},{-1,-1,-1},{-1, 1,-1},
+    { 1,-1, 1},{-1,-1,-1},{ 1,-1,-1}, { 1, 1,-1},{ 1,-1,-1},{-1,-1,-1},
+    {-1,-1,-1},{-1, 1, 1},{-1, 1,-1}, { 1,-1, 1},{-1,-1, 1},{-1,-1,-1},
+    {-1, 1, 1},{-1,-1, 1},{ 1,-1, 1}, { 1, 1, 1},{ 1,-1,-1},{ 1, 1,-1},
+    { 1,-1,-1},{ 1, 1, 1},{ 1,-1, 1}, { 1, 1, 1},{ 1, 1,-1},{-1, 1,-1},
+    { 1, 1, 1},{-1, 1,-1},{-1, 1, 1}, { 1, 1, 1},{-1, 1, 1},{ 1,-1, 1}};
+
+void orc_cube_init(float verts[144]) {
+    for (int i = 0; i < 36; ++i) {
+        verts[4 * i + 0] = (float)kUnitCube[i][0];
+        verts[4 * i + 1] = (float)kUnitCube[i][1];
+        verts[4 * i + 2] = (float)kUnitCube[i][2];
+        verts[4 * i + 3] = 1.0f;
+    }
+}
+
+static void apply(float verts[144], const mat4* m) {
+    for (int i = 0; i < 36; ++i) {
+        float out[4];
+        mat_mul_vec(m, &verts[4 * i], out);
+        memcpy(&verts[4 * i], out, sizeof out);
+    }
+}
+
+/* Cube.cpp:53-63: R = rotate(rotate(rotate(I, z, Z), y, Y), x, X) */
+void orc_cube_rotate(float verts[144], float rx, float ry, float rz) {
+    mat4 I = mat_identity();
+    mat4 m = glm_rotate(&I, rz, 0.0f, 0.0f, 1.0f);
+    m = glm_rotate(&m, ry, 0.0f, 1.0f, 0.0f);
+    m = glm_rotate(&m, rx, 1.0f, 0.0f, 0.0f);
+    apply(verts, &m);
+}
+
+/* Cube.cpp:65-73, glm scale matrix_transform.inl:122-134 */
+void orc_cube_scale(float verts[144], float sx, float sy, float sz) {
+    mat4 I = mat_identity();
+    mat4 m;
+    const float v[3] = {sx, sy, sz};
+    for (int i = 0; i < 3; ++i)
+        for (int r = 0; r < 4; ++r) m.c[i][r] = I.c[i][r] * v[i];
+    for (int r = 0; r < 4; ++r) m.c[3][r] = I.c[3][r];
+    apply(verts, &m);
+}
+
+/* Cube.cpp:75-83, glm translate matrix_transform.inl:40-50:
+ * Result[3] = ((m0*v0 + m1*v1) + m2*v2) + m3 */
+void orc_cube_translate(float verts[144], float tx, float ty, float tz) {
+    mat4 m = mat_identity();
+    for (int r = 0; r < 4; ++r)
+        m.c[3][r] = m.c[0][r] * tx + m.c[1][r] * ty + m.c[2][r] * tz + m.c[3][r];
+    apply(verts, &m);
+}
+
+/* Utility.cpp:343-347 with PI = 3.1415926535f (Utility.h:19) */
+float orc_deg2rad(float deg) { return deg * 3.1415926535f / 180.0f; }
+
+/* MainState.cpp:37-39: perspective(45, 4/3, 0, 100) * (0,0,1,1);
+ * glm matrix_transform.inl:212-231 (radians in 0.9.6). */
+void orc_ray_dir(float out[4]) {
+    const float fovy = 45.0f, aspect = 4.0f / 3.0f, zn = 0.0f, zf = 100.0f;
+    float th = tanf(fovy / 2.0f);
+    mat4 p;
+    memset(&p, 0, sizeof p);
+    p.c[0][0] = 1.0f / (aspect * th);
+    p.c[1][1] = 1.0f / th;
+    p.c[2][2] = -(zf + zn) / (zf - zn);
+    p.c[2][3] = -1.0f;
+    p.c[3][2] = -(2.0f * zf * zn) / (zf - zn);
+    const float v[4] = {0.0f, 0.0f, 1.0f, 1.0f};
+    mat_mul_vec(&p, v, out);
+}
+
+/* ------------------------------------------------------------------------
+ * Random::getFloat, Random.cpp:29-42 (glibc rand())
+ * ---------------------------------------------------------------------- */
+static float rnd(float mn, float mx) {
+    float random = ((float)rand()) / (float)RAND_MAX;
+    float diff = mx - mn;
+    float r = random * diff;
+    return mn + r;
+}
+
+/* Three getFloat() calls that appear as arguments of one constructor call:
+ * the C++ evaluation order is unspecified; rtl selects it. */
+static void rnd3(int rtl, float a0, float b0, float a1, float b1, float a2,
+                 float b2, float out[3]) {
+    if (rtl) {
+        out[2] = rnd(a2, b2);
+        out[1] = rnd(a1, b1);
+        out[0] = rnd(a0, b0);
+    } else {
+        out[0] = rnd(a0, b0);
+        out[1] = rnd(a1, b1);
+        out[2] = rnd(a2, b2);
+    }
+}
+
+typedef struct {
+    float *so, *sr, *sc, *cv, *cc;
+    int ns, nc;
+} scene_sink;
+
+static void add_sphere(scene_sink* s, float x, float y, float z, float w, float r,
+                       float cr, float cg, float cb, float ca) {
+    float* o = s->so + 4 * s->ns;
+    o[0] = x; o[1] = y; o[2] = z; o[3] = w;
+    s->sr[s->ns] = r;
+    float* c = s->sc + 4 * s->ns;
+    c[0] = cr; c[1] = cg; c[2] = cb; c[3] = ca;
+    s->ns++;
+}
+
+static float* new_cube(scene_sink* s, float cr, float cg, float cb, float ca) {
+    float* v = s->cv + 144 * s->nc;
+    orc_cube_init(v);
+    float* c = s->cc + 4 * s->nc;
+    c[0] = cr; c[1] = cg; c[2] = cb; c[3] = ca;
+    s->nc++;
+    return v;
+}
+
+#define D2R orc_deg2rad
+
+/* MainState.cpp:434-461 (shared by scenes 1 and 2) */
+static void fixed_cubes(scene_sink* s) {
+    float* v = new_cube(s, 1.0f, 1.0f, 0.0f, 255.0f);
+    orc_cube_scale(v, 40.0f, 40.0f, 40.0f);
+    orc_cube_rotate(v, 0.0f, 0.0f, D2R(30.0f));
+    orc_cube_rotate(v, 0.0f, D2R(30.0f), 0.0f);
+    orc_cube_translate(v, 70.0f, 60.0f, -60.0f);
+
+    v = new_cube(s, 0.0f, 1.0f, 1.0f, 255.0f);
+    orc_cube_scale(v, 30.0f, 30.0f, 30.0f);
+    orc_cube_rotate(v, 0.0f, 0.0f, D2R(80.0f));
+    orc_cube_rotate(v, 0.0f, D2R(250.0f), 0.0f);
+    orc_cube_translate(v, 150.0f, 60.0f, -70.0f);
+
+    v = new_cube(s, 0.0f, 0.0f, 1.0f, 255.0f);
+    orc_cube_scale(v, 10.0f, 10.0f, 10.0f);
+    orc_cube_rotate(v, 0.0f, 0.0f, D2R(160.0f));
+    orc_cube_rotate(v, D2R(210.0f), 0.0f, 0.0f);
+    orc_cube_translate(v, 150.0f, 400.0f, -40.0f);
+
+    v = new_cube(s, 1.0f, 0.0f, 0.0f, 255.0f);
+    orc_cube_scale(v, 50.0f, 50.0f, 50.0f);
+    orc_cube_rotate(v, 0.0f, 0.0f, D2R(80.0f));
+    orc_cube_rotate(v, 0.0f, D2R(250.0f), 0.0f);
+    orc_cube_translate(v, 450.0f, 200.0f, -80.0f);
+}
+
+/* MainState.cpp:419-432 */
+static void scene1(scene_sink* s) {
+    add_sphere(s, 300.0f, 250.0f, -85.0f, 1.0f, 50.0f, 0.0f, 1.0f, 1.0f, 255.0f);
+    add_sphere(s, 500.0f, 250.0f, -85.0f, 1.0f, 30.0f, 1.0f, 0.0f, 1.0f, 255.0f);
+    fixed_cubes(s);
+}
+
+/* MainState.cpp:464-594 */
+static void scene2(scene_sink* s, int rtl) {
+    static const float o[8][3] = {{100, 150, -85}, {300, 400, -65}, {350, 150, -85},
+                                  {200, 250, -85}, {200, 350, -45}, {600, 450, -125},
+                                  {20, 450, -64},  {620, 250, -115}};
+    static const float r[8] = {50, 30, 15, 25, 20, 42, 42, 32};
+    for (int i = 0; i < 8; ++i) {
+        float c[3];
+        rnd3(rtl, 0.05f, 1.0f, 0.05f, 1.0f, 0.05f, 1.0f, c); /* :487-495 */
+        add_sphere(s, o[i][0], o[i][1], o[i][2], 1.0f, r[i], c[0], c[1], c[2], 255.0f);
+    }
+    fixed_cubes(s); /* cubes 1-4, :499-526 */
+    float c[3];
+    float* v;
+
+    rnd3(rtl, 0.05f, 1.0f, 0.05f, 1.0f, 0.05f, 1.0f, c); /* cube5 :528-537 */
+    v = new_cube(s, c[0], c[1], c[2], 255.0f);
+    orc_cube_scale(v, 30.0f, 30.0f, 30.0f);
+    orc_cube_rotate(v, D2R(170.0f), 0.0f, 0.0f);
+    orc_cube_rotate(v, 0.0f, D2R(150.0f), 0.0f);
+    orc_cube_translate(v, 450.0f, 400.0f, -60.0f);
+
+    rnd3(rtl, 0.05f, 1.0f, 0.05f, 1.0f, 0.05f, 1.0f, c); /* cube6 :539-548 */
+    v = new_cube(s, c[0], c[1], c[2], 255.0f);
+    orc_cube_scale(v, 50.0f, 50.0f, 50.0f);
+    orc_cube_rotate(v, 0.0f, 0.0f, D2R(80.0f));
+    orc_cube_rotate(v, D2R(350.0f), 0.0f, 0.0f);
+    orc_cube_translate(v, 50.0f, 300.0f, -100.0f);
+
+    rnd3(rtl, 0.05f, 1.0f, 0.05f, 1.0f, 0.05f, 1.0f, c); /* cube7 :550-559 */
+    v = new_cube(s, c[0], c[1], c[2], 255.0f);
+    orc_cube_scale(v, 70.0f, 70.0f, 70.0f);
+    orc_cube_rotate(v, D2R(160.0f), 0.0f, 0.0f);
+    orc_cube_rotate(v, 0.0f, D2R(250.0f), 0.0f);
+    orc_cube_translate(v, 530.0f, 300.0f, -100.0f);
+
+    rnd3(rtl, 0.05f, 1.0f, 0.05f, 1.0f, 0.05f, 1.0f, c); /* cube8 :561-570 */
+    v = new_cube(s, c[0], c[1], c[2], 255.0f);
+    orc_cube_scale(v, 25.0f, 25.0f, 25.0f);
+    orc_cube_rotate(v, 0.0f, 0.0f, D2R(190.0f));
+    orc_cube_rotate(v, 0.0f, D2R(140.0f), 0.0f);
+    orc_cube_translate(v, 230.0f, 150.0f, -40.0f);
+
+    rnd3(rtl, 0.05f, 1.0f, 0.05f, 1.0f, 0.05f, 1.0f, c); /* cube9 :572-582 */
+    v = new_cube(s, c[0], c[1], c[2], 255.0f);
+    orc_cube_scale(v, 50.0f, 50.0f, 50.0f);
+    orc_cube_rotate(v, 0.0f, D2R(130.0f), 0.0f);
+    orc_cube_rotate(v, D2R(150.0f), 0.0f, 9.9f); /* 9.9 rad, as written at :579 */
+    orc_cube_rotate(v, 0.0f, 0.0f, D2R(50.0f));
+    orc_cube_translate(v, 510.0f, 50.0f, -90.0f);
+
+    rnd3(rtl, 0.05f, 1.0f, 0.05f, 1.0f, 0.05f, 1.0f, c); /* cube10 :584-593 */
+    v = new_cube(s, c[0], c[1], c[2], 255.0f);
+    orc_cube_scale(v, 24.0f, 24.0f, 24.0f);
+    orc_cube_rotate(v, 0.0f, 0.0f, D2R(280.0f));
+    orc_cube_rotate(v, 0.0f, D2R(20.0f), 0.0f);
+    orc_cube_translate(v, 350.0f, 340.0f, -40.0f);
+}
+
+/* MainState.cpp:596-639 */
+static void scene3(scene_sink* s, int rtl) {
+    for (int i = 0; i < 100; ++i) {
+        float p[3], c[3];
+        /* :601-606 vec4(getFloat(0,630), getFloat(0,470), -getFloat(20,100), 1) */
+        rnd3(rtl, 0.0f, 630.0f, 0.0f, 470.0f, 20.0f, 100.0f, p);
+        float r = rnd(5.0f, 30.0f); /* :608 */
+        rnd3(rtl, 0.05f, 1.0f, 0.05f, 1.0f, 0.05f, 1.0f, c); /* :610-614 */
+        add_sphere(s, p[0], p[1], -p[2], 1.0f, r, c[0], c[1], c[2], 255.0f);
+    }
+    for (int i = 0; i < 100; ++i) {
+        float c[3], t[3];
+        rnd3(rtl, 0.05f, 1.0f, 0.05f, 1.0f, 0.05f, 1.0f, c); /* :619-623 */
+        float* v = new_cube(s, c[0], c[1], c[2], 255.0f);
+        float sc = rnd(5.0f, 30.0f); /* :625 */
+        orc_cube_scale(v, sc, sc, sc);
+        orc_cube_rotate(v, 0.0f, 0.0f, D2R(rnd(0.0f, 359.0f))); /* :627 */
+        orc_cube_rotate(v, 0.0f, D2R(rnd(0.0f, 359.0f)), 0.0f); /* :628 */
+        orc_cube_rotate(v, D2R(rnd(0.0f, 359.0f)), 0.0f, 0.0f); /* :629 */
+        rnd3(rtl, 0.0f, 630.0f, 0.0f, 470.0f, 30.0f, 100.0f, t); /* :631-635 */
+        orc_cube_translate(v, t[0], t[1], -t[2]);
+    }
+}
+
+int orc_scene_reference(int scene_id, unsigned seed, int rtl, float* sphere_origins,
+                        float* sphere_radius, float* sphere_colours,
+                        float* cube_vertices, float* cube_colours, int32_t* n_spheres,
+                        int32_t* n_cubes) {
+    scene_sink s = {sphere_origins, sphere_radius, sphere_colours, cube_vertices,
+                    cube_colours, 0, 0};
+    srand(seed); /* Random::init(seed), Random.cpp:10-17 (seed 0 = time is not used) */
+    switch (scene_id) {
+    case 1: scene1(&s); break;
+    case 2: scene2(&s, rtl); break;
+    case 3: scene3(&s, rtl); break;
+    default: return -1;
+    }
+    *n_spheres = s.ns;
+    *n_cubes = s.nc;
+    return 0;
+}
+
+/* ------------------------------------------------------------------------
+ * Synthetic scene.  Not in the reference: a portable,
+ * seeded restatement of the scene-3 distributions.
+ * ---------------------------------------------------------------------- */
+static uint64_t splitmix64(uint64_t* s) {
+    uint64_t z = (*s += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+static float urand(uint64_t* s, float mn, float mx) {
+    float u = (float)(splitmix64(s) >> 40) * (1.0f / 16777216.0f); /* [0,1) */
+    return mn + u * (mx - mn);
+}
+
+void orc_scene_synthetic(int32_t width, int32_t height, int32_t n_spheres,
+                         int32_t n_cubes, uint64_t seed, float k,
+                         float* sphere_origins, float* sphere_radius,
+                         float* sphere_colours, float* cube_vertices,
+                         float* cube_colours) {
+    uint64_t st = seed;
+    for (int i = 0; i < n_spheres; ++i) {
+        float x = urand(&st, 0.0f, (float)width);
+        float y = urand(&st, 0.0f, (float)height);
+        float z = -urand(&st, 20.0f, 100.0f);
+        float r = urand(&st, 5.0f, 30.0f) * k;
+        float cr = urand(&st, 0.05f, 1.0f);
+        float cg = urand(&st, 0.05f, 1.0f);
+        float cb = urand(&st, 0.05f, 1.0f);
+        float* o = sphere_origins + 4 * i;
+        o[0] = x; o[1] = y; o[2] = z; o[3] = 1.0f;
+        sphere_radius[i] = r;
+        float* c = sphere_colours + 4 * i;
+        c[0] = cr; c[1] = cg; c[2] = cb; c[3] = 255.0f;
+    }
+    for (int i = 0; i < n_cubes; ++i) {
+        float cr = urand(&st, 0.05f, 1.0f);
+        float cg = urand(&st, 0.05f, 1.0f);
+        float cb = urand(&st, 0.05f, 1.0f);
+        float sc = urand(&st, 5.0f, 30.0f) * k;
+        float az = urand(&st, 0.0f, 359.0f);
+        float ay = urand(&st, 0.0f, 359.0f);
+        float ax = urand(&st, 0.0f, 359.0f);
+        float tx = urand(&st, 0.0f, (float)width);
+        float ty = urand(&st, 0.0f, (float)height);
+        float tz = -urand(&st, 30.0f, 100.0f);
+        float* v = cube_vertices + 144 * i;
+        orc_cube_init(v);
+        orc_cube_scale(v, sc, sc, sc);
+        orc_cube_rotate(v, 0.0f, 0.0f, D2R(az));
+        orc_cube_rotate(v, 0.0f, D2R(ay), 0.0f);
+        orc_cube_rotate(v, D2R(ax), 0.0f, 0.0f);
+        orc_cube_translate(v, tx, ty, tz);
+        float* c = cube_colours + 4 * i;
+        c[0] = cr; c[1] = cg; c[2] = cb; c[3] = 255.0f;
+    }
+}
+
+/* ------------------------------------------------------------------------
+ * Hot path, MainState.cpp:16-24 (macros), :257-298, :300-327, :330-408
+ * ---------------------------------------------------------------------- */
+#define EPSILON 0.000001
+#define CROSS(dest, v1, v2)                      \
+    dest[0] = v1[1] * v2[2] - v1[2] * v2[1];     \
+    dest[1] = v1[2] * v2[0] - v1[0] * v2[2];     \
+    dest[2] = v1[0] * v2[1] - v1[1] * v2[0];
+#define DOT(v1, v2) (v1[0] * v2[0] + v1[1] * v2[1] + v1[2] * v2[2])
+#define SUB(dest, v1, v2)  \
+    dest[0] = v1[0] - v2[0]; \
+    dest[1] = v1[1] - v2[1]; \
+    dest[2] = v1[2] - v2[2];
+
+/* MainState.cpp:257-298 (fp64 Moller-Trumbore, no t > 0 test) */
+int orc_intersect_tri(const double orig[3], const double dir[3], const double vert0[3],
+                      const double vert1[3], const double vert2[3], double* t, double* u,
+                      double* v) {
+    double edge1[3], edge2[3], tvec[3], pvec[3], qvec[3];
+    double det, inv_det;
+    SUB(edge1, vert1, vert0);
+    SUB(edge2, vert2, vert0);
+    CROSS(pvec, dir, edge2);
+    det = DOT(edge1, pvec);
+    if (det > -EPSILON && det < EPSILON) return 0;
+    inv_det = 1.0 / det;
+    SUB(tvec, orig, vert0);
+    *u = DOT(tvec, pvec) * inv_det;
+    if (*u < 0.0 || *u > 1.0) return 0;
+    CROSS(qvec, tvec, edge1);
+    *v = DOT(dir, qvec) * inv_det;
+    if (*v < 0.0 || *u + *v > 1.0) return 0;
+    *t = DOT(edge2, qvec) * inv_det;
+    return 1;
+}
+
+/* glm vec4 dot: (x0y0 + x1y1) + (x2y2 + x3y3), func_geometric.inl:75-81 */
+static float dot4(const float a[4], const float b[4]) {
+    float t0 = a[0] * b[0], t1 = a[1] * b[1], t2 = a[2] * b[2], t3 = a[3] * b[3];
+    return (t0 + t1) + (t2 + t3);
+}
+
+/* MainState.cpp:300-327 (fp32 through glm) */
+float orc_intersect_sphere(const float o[4], const float d[4], float radius,
+                           const float c[4]) {
+    float L[4] = {c[0] - o[0], c[1] - o[1], c[2] - o[2], c[3] - o[3]};
+    float tca = dot4(L, d);
+    if (tca < 0) return 0.0f;
+    float distanceSquared = dot4(L, L) - tca * tca;
+    float radiusSquared = radius * radius;
+    if (distanceSquared > radiusSquared) return 0.0f;
+    float thc = sqrtf(radiusSquared - distanceSquared);
+    float t0 = tca - thc;
+    return t0;
+}
+
+/* (int)f as x86-64 cvttss2si computes it (MainState.cpp:952-955):
+ * truncation toward zero; NaN / out of range -> INT32_MIN. */
+static int32_t cvt_i32(float f) {
+    if (f >= -2147483648.0f && f < 2147483648.0f) return (int32_t)f;
+    return INT32_MIN;
+}
+
+/* MainState.cpp:330-408 */
+void orc_collide(const float origin[4], const float dir[4], int32_t n_spheres,
+                 const float* sphere_origins, const float* sphere_radius,
+                 const float* sphere_colours, int32_t n_cubes, const float* cube_vertices,
+                 const float* cube_colours, int32_t out[4]) {
+    double rayOrigin[3] = {origin[0], origin[1], origin[2]};
+    double rayDirection[3] = {dir[0], dir[1], dir[2]};
+    double tri0[3], tri1[3], tri2[3];
+    double t = 0, u = 0, v = 0;
+    float colour[4] = {0.0f, 0.0f, 0.0f, 255.0f};
+    float closest = 300000.0f;
+
+    for (int c = 0; c < n_cubes; ++c) { /* :348-377 */
+        const float* tris = cube_vertices + 144 * c;
+        for (int tri = 0; tri < 36; tri += 3) {
+            for (int k = 0; k < 3; ++k) {
+                tri0[k] = tris[4 * tri + k];
+                tri1[k] = tris[4 * (tri + 1) + k];
+                tri2[k] = tris[4 * (tri + 2) + k];
+            }
+            if (orc_intersect_tri(rayOrigin, rayDirection, tri0, tri1, tri2, &t, &u, &v) == 1) {
+                if ((float)t < closest) {
+                    closest = (float)t;
+                    memcpy(colour, cube_colours + 4 * c, sizeof colour);
+                }
+            }
+        }
+    }
+    for (int s = 0; s < n_spheres; ++s) { /* :382-394 */
+        float distance = orc_intersect_sphere(origin, dir, sphere_radius[s],
+                                              sphere_origins + 4 * s);
+        if (distance == 0.0f) continue;
+        if (distance < closest) {
+            closest = distance;
+            memcpy(colour, sphere_colours + 4 * s, sizeof colour);
+        }
+    }
+    if (closest == 300000.0f) { /* :397-400 */
+        out[0] = 0; out[1] = 0; out[2] = 0; out[3] = 255;
+        return;
+    }
+    /* :403-406, normaliseFloat(closest, 180, 0) = (closest - 0)/(180 - 0) */
+    float normalised = (closest - 0.0f) / (180.0f - 0.0f);
+    float colourScalar = 255.0f - (normalised * 255.0f);
+    out[0] = cvt_i32(colourScalar * colour[0]);
+    out[1] = cvt_i32(colourScalar * colour[1]);
+    out[2] = cvt_i32(colourScalar * colour[2]);
+    out[3] = 255;
+}
+
+/* MainState.cpp:936-956 */
+void orc_trace(int32_t width, int32_t height, int32_t row_begin, int32_t row_end,
+               const float ray_dir[4], const float* ray_origins, int32_t n_spheres,
+               const float* sphere_origins, const float* sphere_radius,
+               const float* sphere_colours, int32_t n_cubes, const float* cube_vertices,
+               const float* cube_colours, int32_t* out) {
+    (void)height;
+    for (int32_t y = row_begin; y < row_end; ++y) {
+        for (int32_t x = 0; x < width; ++x) {
+            float o[4];
+            int64_t gi = (int64_t)y * width + x;
+            if (ray_origins) {
+                memcpy(o, ray_origins + 4 * gi, sizeof o);
+            } else { /* MainState.cpp:44-50 */
+                o[0] = (float)x; o[1] = (float)y; o[2] = 0.0f; o[3] = 1.0f;
+            }
+            orc_collide(o, ray_dir, n_spheres, sphere_origins, sphere_radius,
+                        sphere_colours, n_cubes, cube_vertices, cube_colours,
+                        out + 4 * ((int64_t)(y - row_begin) * width + x));
+        }
+    }
+}
+
+typedef struct {
+    int32_t width, height, row_begin, row_end, stride, phase;
+    const float *ray_dir, *ray_origins;
+    int32_t n_spheres, n_cubes;
+    const float *so, *sr, *sc, *cv, *cc;
+    int32_t* out;
+} mt_job;
+
+static void* mt_worker(void* arg) {
+    mt_job* j = (mt_job*)arg;
+    for (int32_t y = j->row_begin + j->phase; y < j->row_end; y += j->stride)
+        orc_trace(j->width, j->height, y, y + 1, j->ray_dir, j->ray_origins, j->n_spheres,
+                  j->so, j->sr, j->sc, j->n_cubes, j->cv, j->cc,
+                  j->out + 4 * (int64_t)(y - j->row_begin) * j->width);
+    return NULL;
+}
+
+void orc_trace_mt(int32_t width, int32_t height, int32_t row_begin, int32_t row_end,
+                  const float ray_dir[4], const float* ray_origins, int32_t n_spheres,
+                  const float* sphere_origins, const float* sphere_radius,
+                  const float* sphere_colours, int32_t n_cubes, const float* cube_vertices,
+                  const float* cube_colours, int32_t* out, int32_t n_threads) {
+    if (n_threads < 1) n_threads = 1;
+    if (n_threads > 256) n_threads = 256;
+    pthread_t th[256];
+    mt_job jobs[256];
+    for (int i = 0; i < n_threads; ++i) {
+        mt_job j = {width, height, row_begin, row_end, n_threads, i, ray_dir, ray_origins,
+                    n_spheres, n_cubes, sphere_origins, sphere_radius, sphere_colours,
+                    cube_vertices, cube_colours, out};
+        jobs[i] = j;
+        pthread_create(&th[i], NULL, mt_worker, &jobs[i]);
+    }
+    for (int i = 0; i < n_threads; ++i) pthread_join(th[i], NULL);
+}
+
+uint64_t orc_fnv1a_i32(const int32_t* v, int64_t n) {
+    uint64_t h = 0xcbf29ce484222325ull;
+    for (int64_t i = 0; i < n; ++i) {
+        h ^= (uint32_t)v[i];
+        h *= 0x100000001b3ull;
+    }
+    return h;
+}
+
+void orc_pack_rgba8(const int32_t* frame, int64_t n_pixels, uint32_t* out) {
+    for (int64_t i = 0; i < n_pixels; ++i) {
+        uint32_t r = (uint8_t)frame[4 * i + 0];
+        uint32_t g = (uint8_t)frame[4 * i + 1];
+        uint32_t b = (uint8_t)frame[4 * i + 2];
+        out[i] = r | (g << 8) | (b << 16) | 0xFF000000u;
+    }
+}
+
+/* ------------------------------------------------------------------------
+ * The reference's own OpenCL kernel semantics, rayTracer.cl:37-202, for the
+ * record only: its fp32 Moller-Trumbore disagrees with the
+ * CPU path on silhouette pixels.  The parity target is orc_trace above; the
+ * tests use this to pin the restatement against the survey's probe counts.
+ * ---------------------------------------------------------------------- */
+static int cl_intersect_tri(const float orig[3], const float dir[3], const float vert0[3],
+                            const float vert1[3], const float vert2[3], float* t, float* u,
+                            float* v) {
+    float edge1[3], edge2[3], tvec[3], pvec[3], qvec[3];
+    float det, inv_det;
+    SUB(edge1, vert1, vert0);
+    SUB(edge2, vert2, vert0);
+    CROSS(pvec, dir, edge2);
+    det = DOT(edge1, pvec);
+    if (det > -EPSILON && det < EPSILON) return 0; /* double compare, :54 */
+    inv_det = 1.0 / det;                            /* double literal, :56 */
+    SUB(tvec, orig, vert0);
+    *u = DOT(tvec, pvec) * inv_det;
+    if (*u < 0.0 || *u > 1.0) return 0;
+    CROSS(qvec, tvec, edge1);
+    *v = DOT(dir, qvec) * inv_det;
+    if (*v < 0.0 || *u + *v > 1.0) return 0;
+    *t = DOT(edge2, qvec) * inv_det;
+    return 1;
+}
+
+void orc_trace_cl32(int32_t width, int32_t height, const float ray_dir[4], int32_t n_spheres,
+                    const float* sphere_origins, const float* sphere_radius,
+                    const float* sphere_colours, int32_t n_cubes, const float* cube_vertices,
+                    const float* cube_colours, int32_t* out) {
+    for (int32_t y = 0; y < height; ++y) {
+        for (int32_t x = 0; x < width; ++x) {
+            const float o[4] = {(float)x, (float)y, 0.0f, 1.0f};
+            const float oc[3] = {o[0], o[1], o[2]}, dc[3] = {ray_dir[0], ray_dir[1], ray_dir[2]};
+            float closest = 300000.0f, colour[4] = {0.0f, 0.0f, 0.0f, 255.0f};
+            float t = 0, u = 0, v = 0;
+            for (int c = 0; c < n_cubes; ++c) {
+                for (int tri = 0; tri < 36; tri += 3) {
+                    float a[3], b[3], e[3];
+                    for (int k = 0; k < 3; ++k) {
+                        a[k] = cube_vertices[144 * c + 4 * tri + k];
+                        b[k] = cube_vertices[144 * c + 4 * (tri + 1) + k];
+                        e[k] = cube_vertices[144 * c + 4 * (tri + 2) + k];
+                    }
+                    if (cl_intersect_tri(oc, dc, a, b, e, &t, &u, &v) == 1 && t < closest) {
+                        closest = t;
+                        memcpy(colour, cube_colours + 4 * c, sizeof colour);
+                    }
+                }
+            }
+            for (int s = 0; s < n_spheres; ++s) {
+                float d = orc_intersect_sphere(o, ray_dir, sphere_radius[s], sphere_origins + 4 * s);
+                if (d == 0.0f) continue;
+                if (d < closest) {
+                    closest = d;
+                    memcpy(colour, sphere_colours + 4 * s, sizeof colour);
+                }
+            }
+            int32_t* p = out + 4 * ((int64_t)y * width + x);
+            if (closest == 300000.0f) {
+                p[0] = 0; p[1] = 0; p[2] = 0; p[3] = 255;
+                continue;
+            }
+            float sc = 255.0f - ((closest - 0.0f) / (180.0f - 0.0f)) * 255.0f;
+            p[0] = cvt_i32(sc * colour[0]);
+            p[1] = cvt_i32(sc * colour[1]);
+            p[2] = cvt_i32(sc * colour[2]);
+            p[3] = 255;
+        }
+    }
+}

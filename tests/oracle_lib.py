@@ -1,0 +1,187 @@
+"""ctypes wrapper of oracle/liboracle.so -- TEST INFRASTRUCTURE ONLY.
+
+The oracle is the CPU restatement of the reference's serial ray tracer
+(oracle/rt_oracle.c).  Only tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg use it, and only as the checker / CPU baseline.
+"""
+from __future__ import annotations
+
+import ctypes
+import subprocess
+from pathlib import Path
+from types import SimpleNamespace
+from typing import Optional, Tuple
+
+import numpy as np
+
+REPO = Path(__file__).resolve().parents[1]
+ORACLE_DIR = REPO / "oracle"
+LIB = ORACLE_DIR / "liboracle.so"
+REF_LIB = ORACLE_DIR / "_ref" / "libref_cube.so"
+
+_vp, _i32, _f32 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_float
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data
+
+
+def _load() -> ctypes.CDLL:
+    if not LIB.exists():
+        subprocess.run(["make", "-C", str(ORACLE_DIR), "all"], check=True)
+    lib = ctypes.CDLL(str(LIB))
+    sig = {
+        "orc_cube_init": (None, [_vp]),
+        "orc_cube_scale": (None, [_vp, _f32, _f32, _f32]),
+        "orc_cube_rotate": (None, [_vp, _f32, _f32, _f32]),
+        "orc_cube_translate": (None, [_vp, _f32, _f32, _f32]),
+        "orc_deg2rad": (_f32, [_f32]),
+        "orc_ray_dir": (None, [_vp]),
+        "orc_scene_reference": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint, ctypes.c_int, _vp,
+                                               _vp, _vp, _vp, _vp, ctypes.POINTER(_i32),
+                                               ctypes.POINTER(_i32)]),
+        "orc_scene_synthetic": (None, [_i32, _i32, _i32, _i32, ctypes.c_uint64, _f32, _vp, _vp,
+                                       _vp, _vp, _vp]),
+        "orc_intersect_tri": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+        "orc_intersect_sphere": (_f32, [_vp, _vp, _f32, _vp]),
+        "orc_trace": (None, [_i32, _i32, _i32, _i32, _vp, _vp, _i32, _vp, _vp, _vp, _i32, _vp,
+                             _vp, _vp]),
+        "orc_trace_mt": (None, [_i32, _i32, _i32, _i32, _vp, _vp, _i32, _vp, _vp, _vp, _i32, _vp,
+                                _vp, _vp, _i32]),
+        "orc_trace_cl32": (None, [_i32, _i32, _vp, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _vp]),
+        "orc_fnv1a_i32": (ctypes.c_uint64, [_vp, ctypes.c_int64]),
+        "orc_pack_rgba8": (None, [_vp, ctypes.c_int64, _vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+class Oracle:
+    _lib: Optional[ctypes.CDLL] = None
+
+    def __init__(self):
+        if Oracle._lib is None:
+            Oracle._lib = _load()
+        self.lib = Oracle._lib
+
+    # ---- scenes -----------------------------------------------------------
+    def scene_reference(self, scene_id: int, seed: int = 1, rtl: int = 1) -> SimpleNamespace:
+        so = np.zeros((100, 4), np.float32)
+        sr = np.zeros(100, np.float32)
+        sc = np.zeros((100, 4), np.float32)
+        cv = np.zeros((100, 36, 4), np.float32)
+        cc = np.zeros((100, 4), np.float32)
+        ns, nc = _i32(), _i32()
+        rc = self.lib.orc_scene_reference(scene_id, seed, rtl, _p(so), _p(sr), _p(sc), _p(cv),
+                                          _p(cc), ctypes.byref(ns), ctypes.byref(nc))
+        assert rc == 0
+        n, m = ns.value, nc.value
+        return SimpleNamespace(sphere_origins=so[:n].copy(), sphere_radius=sr[:n].copy(),
+                               sphere_colours=sc[:n].copy(), cube_vertices=cv[:m].copy(),
+                               cube_colours=cc[:m].copy())
+
+    def scene_synthetic(self, width, height, n, m, seed, k) -> SimpleNamespace:
+        so = np.zeros((n, 4), np.float32)
+        sr = np.zeros(n, np.float32)
+        sc = np.zeros((n, 4), np.float32)
+        cv = np.zeros((m, 36, 4), np.float32)
+        cc = np.zeros((m, 4), np.float32)
+        self.lib.orc_scene_synthetic(width, height, n, m, seed, k, _p(so), _p(sr), _p(sc),
+                                     _p(cv), _p(cc))
+        return SimpleNamespace(sphere_origins=so, sphere_radius=sr, sphere_colours=sc,
+                               cube_vertices=cv, cube_colours=cc)
+
+    def ray_dir(self) -> np.ndarray:
+        d = np.zeros(4, np.float32)
+        self.lib.orc_ray_dir(_p(d))
+        return d
+
+    # ---- tracing ----------------------------------------------------------
+    @staticmethod
+    def _arrays(scene):
+        c = lambda a, shape: np.ascontiguousarray(a, np.float32).reshape(shape)
+        return (c(scene.sphere_origins, (-1, 4)), c(scene.sphere_radius, (-1,)),
+                c(scene.sphere_colours, (-1, 4)), c(scene.cube_vertices, (-1, 36, 4)),
+                c(scene.cube_colours, (-1, 4)))
+
+    def trace(self, scene, width: int, height: int, rows: Optional[Tuple[int, int]] = None,
+              ray_dir: Optional[np.ndarray] = None, ray_origins: Optional[np.ndarray] = None,
+              threads: int = 1) -> np.ndarray:
+        rb, re = rows if rows is not None else (0, height)
+        so, sr, sc, cv, cc = self._arrays(scene)
+        d = self.ray_dir() if ray_dir is None else np.ascontiguousarray(ray_dir, np.float32)
+        org = None if ray_origins is None else np.ascontiguousarray(ray_origins, np.float32)
+        out = np.zeros((re - rb, width, 4), np.int32)
+        if threads > 1:
+            self.lib.orc_trace_mt(width, height, rb, re, _p(d), _p(org), len(sr), _p(so), _p(sr),
+                                  _p(sc), len(cc), _p(cv), _p(cc), _p(out), threads)
+        else:
+            self.lib.orc_trace(width, height, rb, re, _p(d), _p(org), len(sr), _p(so), _p(sr),
+                               _p(sc), len(cc), _p(cv), _p(cc), _p(out))
+        return out
+
+    def trace_cl32(self, scene, width: int, height: int) -> np.ndarray:
+        so, sr, sc, cv, cc = self._arrays(scene)
+        out = np.zeros((height, width, 4), np.int32)
+        self.lib.orc_trace_cl32(width, height, _p(self.ray_dir()), len(sr), _p(so), _p(sr),
+                                _p(sc), len(cc), _p(cv), _p(cc), _p(out))
+        return out
+
+    def fnv(self, frame: np.ndarray) -> int:
+        f = np.ascontiguousarray(frame, np.int32)
+        return int(self.lib.orc_fnv1a_i32(_p(f), f.size))
+
+    def pack_rgba8(self, frame: np.ndarray) -> np.ndarray:
+        f = np.ascontiguousarray(frame, np.int32)
+        out = np.zeros(f.shape[:-1], np.uint32)
+        self.lib.orc_pack_rgba8(_p(f), f.size // 4, _p(out))
+        return out
+
+    # ---- primitives -------------------------------------------------------
+    def intersect_tri(self, orig, direction, v0, v1, v2):
+        a = [np.ascontiguousarray(x, np.float64) for x in (orig, direction, v0, v1, v2)]
+        t, u, v = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        hit = self.lib.orc_intersect_tri(*[_p(x) for x in a], ctypes.byref(t), ctypes.byref(u),
+                                         ctypes.byref(v))
+        return hit, t.value
+
+    def intersect_sphere(self, origin, direction, radius, centre) -> float:
+        o = np.ascontiguousarray(origin, np.float32)
+        d = np.ascontiguousarray(direction, np.float32)
+        c = np.ascontiguousarray(centre, np.float32)
+        return float(self.lib.orc_intersect_sphere(_p(o), _p(d), radius, _p(c)))
+
+    def cube(self, ops) -> np.ndarray:
+        v = np.zeros((36, 4), np.float32)
+        self.lib.orc_cube_init(_p(v))
+        fn = {"scale": self.lib.orc_cube_scale, "rotate": self.lib.orc_cube_rotate,
+              "translate": self.lib.orc_cube_translate}
+        for op, x, y, z in ops:
+            fn[op](_p(v), x, y, z)
+        return v
+
+    def deg2rad(self, d: float) -> float:
+        return float(self.lib.orc_deg2rad(d))
+
+
+def ref_cube_lib() -> Optional[ctypes.CDLL]:
+    """oracle/_ref/libref_cube.so: the reference's own Cube.cpp (or None)."""
+    if not REF_LIB.exists():
+        return None
+    lib = ctypes.CDLL(str(REF_LIB))
+    lib.ref_cube_build.restype = ctypes.c_int
+    lib.ref_cube_build.argtypes = [_vp, ctypes.c_int, _vp, _vp, _vp]
+    return lib
+
+
+def ref_cube(lib, colour, ops) -> Tuple[np.ndarray, np.ndarray]:
+    kinds = {"scale": 0, "rotate": 1, "translate": 2}
+    o = np.array([[kinds[k], x, y, z] for k, x, y, z in ops], np.float32).reshape(-1, 4)
+    col = np.asarray(colour, np.float32)
+    v = np.zeros((36, 4), np.float32)
+    c = np.zeros(4, np.float32)
+    assert lib.ref_cube_build(_p(col), len(o), _p(o), _p(v), _p(c)) == 0
+    return v, c

@@ -1,0 +1,242 @@
+"""GPU parity: librt_hip.so (through the C ABI) vs the oracle and the golden
+fixtures, bit-exact on the int32x4 frame (the reference's pixels vector,
+MainState.cpp:952-955).  Run on an MI355X with `pytest -m gpu`."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, golden_scene, load_golden
+
+pytestmark = pytest.mark.gpu
+
+THREADS = min(16, os.cpu_count() or 1)
+SMALL_FIXTURES = ["scene1_640x480", "scene2_640x480", "scene3_640x480", "config1_512x512",
+                  "config2_1920x1080", "config2s_1920x1080"]
+
+
+def diff_report(got, want):
+    bad = (got != want).any(-1) if got.ndim == 3 else (got != want)
+    n = int(bad.sum())
+    if n:
+        ys, xs = np.nonzero(bad)
+        return f"{n} pixels differ, first at (x={xs[0]}, y={ys[0]}): {got[ys[0], xs[0]]} vs {want[ys[0], xs[0]]}"
+    return ""
+
+
+def test_fp32_selftest(rt):
+    """sqrtf and '/' on the device must be the correctly rounded IEEE ops the
+    reference's x86 build uses (sphere thc, MainState.cpp:318; shade :403)."""
+    rng = np.random.default_rng(0)
+    x = np.concatenate([
+        rng.uniform(0, 1e5, 1 << 20).astype(np.float32),
+        rng.uniform(-1e3, 1e3, 1 << 18).astype(np.float32),
+        (rng.standard_normal(1 << 18) * 1e-38).astype(np.float32),  # denormals
+        np.array([0.0, -0.0, 1.0, 2.0, 180.0, 3.4e38, 1e-45], np.float32),
+    ])
+    s, q = rt.selftest_fp32(x)
+    with np.errstate(invalid="ignore"):
+        want_s = np.sqrt(x)
+    want_q = x / np.float32(180.0)
+    assert np.array_equal(s.view(np.uint32)[x >= 0], want_s.view(np.uint32)[x >= 0])
+    assert np.isnan(s[x < 0]).all()
+    assert np.array_equal(q.view(np.uint32), want_q.view(np.uint32))
+
+
+@pytest.mark.parametrize("name", SMALL_FIXTURES)
+@pytest.mark.parametrize("path", ["binned", "generic"])
+def test_golden_frame(pkg, rt, name, path):
+    g = load_golden(name)
+    scene = golden_scene(pkg, g)
+    w, h = int(g["width"]), int(g["height"])
+    frame, t = rt.render(scene, w, h, ray_dir=g["ray_dir"], path=path)
+    assert t.path == path
+    assert not diff_report(frame, g["frame"]), diff_report(frame, g["frame"])
+
+
+@pytest.mark.parametrize("name", ["scene1_640x480", "scene3_640x480", "config2_1920x1080"])
+def test_rgba8_texture(pkg, rt, oracle, name):
+    """The Texture packing (MainState.cpp:1023-1037) produced on the device."""
+    g = load_golden(name)
+    w, h = int(g["width"]), int(g["height"])
+    got, _ = rt.render(golden_scene(pkg, g), w, h, fmt="rgba8")
+    want = oracle.pack_rgba8(g["frame"])
+    assert np.array_equal(got, want)
+
+
+def test_row_bands_assemble(pkg, rt):
+    g = load_golden("scene3_640x480")
+    scene = golden_scene(pkg, g)
+    bands = [(0, 100), (100, 333), (333, 347), (347, 480)]
+    parts = [rt.render(scene, 640, 480, rows=b)[0] for b in bands]
+    assert np.array_equal(np.concatenate(parts), g["frame"])
+
+
+def test_explicit_origins_match(pkg, rt):
+    """The reference uploads rayOrigins (MainState.cpp:44-50, :841-855);
+    passing them explicitly takes the generic kernel and must agree."""
+    g = load_golden("scene2_640x480")
+    ys, xs = np.mgrid[0:480, 0:640]
+    org = np.stack([xs, ys, np.zeros_like(xs), np.ones_like(xs)], -1).astype(np.float32)
+    frame, t = rt.render(golden_scene(pkg, g), 640, 480, ray_origins=org)
+    assert t.path == "generic"
+    assert np.array_equal(frame, g["frame"])
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_general_rays_vs_oracle(pkg, rt, oracle, seed):
+    """Arbitrary directions and origins (kernel args 8-9 in full generality)."""
+    rng = np.random.default_rng(seed)
+    w, h = 96, 72
+    scene = pkg.Scene.synthetic(w, h, 12, 6, seed=seed, k=0.3)
+    d = np.array([rng.uniform(-0.4, 0.4), rng.uniform(-0.4, 0.4), -1.0, -1.0], np.float32)
+    org = np.zeros((h, w, 4), np.float32)
+    org[..., 0] = np.arange(w)[None, :] + rng.uniform(-0.5, 0.5, (h, w))
+    org[..., 1] = np.arange(h)[:, None] + rng.uniform(-0.5, 0.5, (h, w))
+    org[..., 2] = rng.uniform(-5, 5, (h, w))
+    org[..., 3] = 1.0
+    for origins in (None, org):
+        got, t = rt.render(scene, w, h, ray_dir=d, ray_origins=origins)
+        assert t.path == "generic"
+        want = oracle.trace(scene, w, h, ray_dir=d, ray_origins=origins)
+        assert not diff_report(got, want), diff_report(got, want)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_dense_synthetic_vs_oracle(pkg, rt, oracle, seed):
+    """Dense random scenes at awkward sizes (not multiples of the 32x32 bin)."""
+    w, h = 333 + 17 * seed, 257 - 9 * seed
+    scene = pkg.Scene.synthetic(w, h, 40 + 10 * seed, 12 + 4 * seed, seed=100 + seed,
+                                k=w / 640 * (1 + seed % 3))
+    got, t = rt.render(scene, w, h)
+    assert t.path == "binned"
+    want = oracle.trace(scene, w, h, threads=THREADS)
+    assert not diff_report(got, want), diff_report(got, want)
+
+
+def _scene_from(pkg, spheres=(), cubes=()):
+    so = np.array([s[0] for s in spheres], np.float32).reshape(-1, 4)
+    sr = np.array([s[1] for s in spheres], np.float32)
+    sc = np.array([s[2] for s in spheres], np.float32).reshape(-1, 4)
+    cv = np.array([pkg.cube_packed(c[0]) for c in cubes], np.float32).reshape(-1, 36, 4)
+    cc = np.array([c[1] for c in cubes], np.float32).reshape(-1, 4)
+    return pkg.Scene(so, sr, sc, cv, cc)
+
+
+EDGE_CASES = {
+    "empty": dict(),
+    "spheres_only": dict(spheres=[((40, 30, -50, 1), 20, (1, .5, .25, 255)),
+                                  ((60, 30, -20, 1), 25, (.1, .9, .3, 255))]),
+    "cubes_only": dict(cubes=[([("scale", 15, 15, 15), ("rotate", .3, .7, .1),
+                                ("translate", 50, 35, -40)], (.2, .4, .9, 255))]),
+    # origin inside a sphere and cubes crossing z = 0: t < 0, values > 255
+    "behind_origin": dict(spheres=[((50, 40, -10, 1), 40, (1, 1, 1, 255))],
+                          cubes=[([("scale", 30, 30, 30), ("rotate", .5, .2, .9),
+                                   ("translate", 30, 30, 5)], (1, .5, 1, 255))]),
+    # far objects: shade < 0, negative int channels
+    "far": dict(spheres=[((50, 40, -900, 1), 30, (1, 1, 1, 255))],
+                cubes=[([("scale", 20, 20, 20), ("rotate", .1, .2, .3),
+                         ("translate", 20, 20, -2000)], (1, 1, 1, 255))]),
+    # spheres in front of the origin plane never hit (tca < 0), and off-screen
+    "culled": dict(spheres=[((50, 40, 30, 1), 30, (1, 1, 1, 255)),
+                            ((-500, 40, -30, 1), 30, (1, 1, 1, 255)),
+                            ((50, 4000, -30, 1), 30, (1, 1, 1, 255))]),
+    # edge-on slivers: |det| near EPSILON, culling bound must stay conservative
+    "slivers": dict(cubes=[([("scale", 40, 1e-3, 40), ("translate", 50, 40.5, -30)],
+                            (1, .2, .2, 255)),
+                           ([("scale", 40, 1e-3, 40), ("rotate", 1e-4, 0, 0.3),
+                             ("translate", 50, 30, -30)], (1, .6, .2, 255)),
+                           ([("scale", 1e-4, 30, 30), ("rotate", 0, 1e-5, 0),
+                             ("translate", 30, 20, -30)], (.2, 1, .2, 255)),
+                           ([("scale", 3e-3, 3e-3, 3e-3), ("translate", 10, 10, -5)],
+                            (.7, .7, .2, 255)),
+                           ([("scale", 25, 25, 2e-6), ("translate", 70, 50, -30)],
+                            (.2, .2, 1, 255))]),
+    # exact ties: identical spheres / duplicate cubes, first primitive must win
+    "ties": dict(spheres=[((50, 40, -50, 1), 20, (1, 0, 0, 255)),
+                          ((50, 40, -50, 1), 20, (0, 1, 0, 255))],
+                 cubes=[([("scale", 10, 10, 10), ("translate", 20, 20, -30)], (0, 0, 1, 255)),
+                        ([("scale", 10, 10, 10), ("translate", 20, 20, -30)], (1, 1, 0, 255))]),
+    # sphere origin w != 1 and a zero radius
+    "odd_w": dict(spheres=[((50, 40, -50, 3), 20, (1, .3, .3, 255)),
+                           ((20, 20, -50, 1), 0, (1, 1, 1, 255))]),
+}
+
+
+@pytest.mark.parametrize("case", sorted(EDGE_CASES))
+@pytest.mark.parametrize("size", [(101, 77), (1, 1), (64, 64)])
+def test_edge_cases(pkg, rt, oracle, case, size):
+    w, h = size
+    scene = _scene_from(pkg, **EDGE_CASES[case])
+    for path in ("binned", "generic"):
+        got, _ = rt.render(scene, w, h, path=path)
+        want = oracle.trace(scene, w, h)
+        assert not diff_report(got, want), f"{path}: {diff_report(got, want)}"
+
+
+def test_nonfinite_scene_falls_back_exactly(pkg, rt, oracle):
+    """NaN / inf scene data: the binned launch detects it on the device and
+    runs the verbatim reference algorithm (no CPU fallback)."""
+    scene = _scene_from(pkg, spheres=[((30, 30, -40, 1), np.inf, (1, .5, .5, 255)),
+                                      ((60, 30, -40, 1), 10, (.5, 1, .5, 255))],
+                        cubes=[([("scale", 10, 10, 10), ("translate", 40, 40, -30)],
+                                (.5, .5, 1, 255))])
+    scene.cube_vertices[0, 4, 0] = np.nan
+    got, t = rt.render(scene, 90, 70)
+    assert t.path == "binned"
+    want = oracle.trace(scene, 90, 70)
+    assert np.array_equal(got, want)
+
+
+def test_deterministic(pkg, rt):
+    scene = pkg.Scene.synthetic(1024, 768, 128, 32, seed=9, k=1.6)
+    a, _ = rt.render(scene, 1024, 768)
+    b, _ = rt.render(scene, 1024, 768)
+    assert np.array_equal(a, b)
+
+
+def test_lights_do_not_change_pixels(pkg, rt):
+    """The reference has no lighting model (MainState.h:97-106): lights are
+    carried through the ABI and must not affect the frame."""
+    s0 = pkg.Scene.synthetic(256, 200, 16, 4, seed=2, k=0.8, n_lights=0)
+    s2 = pkg.Scene.synthetic(256, 200, 16, 4, seed=2, k=0.8, n_lights=2)
+    assert np.array_equal(rt.render(s0, 256, 200)[0], rt.render(s2, 256, 200)[0])
+
+
+def test_config3_full_frame(pkg, rt, oracle):
+    """BASELINE config 3 at full size (4096^2, 256 spheres + 64 cubes, dense):
+    the full-frame FNV-1a-64 equals the oracle's (fixture), band renders
+    assemble to the same frame, and a row sample matches the oracle."""
+    path = GOLDEN / "config3_4096x4096.npz"
+    if not path.exists():
+        pytest.skip("config3 fixture not generated")
+    g = load_golden("config3_4096x4096")
+    scene = golden_scene(pkg, g)
+    w, h = int(g["width"]), int(g["height"])
+    frame, t = rt.render(scene, w, h)
+    assert t.path == "binned"
+    assert oracle.fnv(frame) == int(g["fnv1a64"])
+    half, _ = rt.render(scene, w, h, rows=(1000, 3000))
+    assert np.array_equal(half, frame[1000:3000])
+    rows = list(range(0, h, 256)) + [h - 1]
+    for r in rows[::4]:
+        want = oracle.trace(scene, w, h, rows=(r, r + 1))
+        assert np.array_equal(frame[r:r + 1], want), f"row {r}"
+
+
+def test_device_api_into_torch(pkg, rt):
+    """rt_render_device writing into a torch tensor on the current stream."""
+    torch = pytest.importorskip("torch")
+    g = load_golden("scene1_640x480")
+    scene = golden_scene(pkg, g)
+    dev = torch.device("cuda:0")
+    t = {k: torch.from_numpy(np.ascontiguousarray(getattr(scene, k))).to(dev)
+         for k in ("sphere_origins", "sphere_radius", "sphere_colours", "cube_vertices",
+                   "cube_colours")}
+    ds = {k: v.data_ptr() for k, v in t.items()}
+    ds.update(num_spheres=scene.num_spheres, num_cubes=scene.num_cubes)
+    out = torch.empty((480, 640, 4), dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream().cuda_stream
+    rt.render_device(ds, 640, 480, (0, 480), out.data_ptr(), stream=stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), g["frame"])
