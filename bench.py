@@ -95,7 +95,10 @@ def main():
         out = torch.empty((rows, w, 4), dtype=torch.int32, device=dev)
     else:
         out = torch.empty((rows, w), dtype=torch.int32, device=dev)
-    stream = torch.cuda.current_stream(dev)
+    # A real stream object: the legacy default stream's handle is 0, which the
+    # C ABI reads as "the context's own stream".
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
 
     def step():
         rt.render_device(dscene, w, full_h, (rb, re), out.data_ptr(), fmt=args.format,
@@ -181,13 +184,13 @@ def main():
         orc = Oracle()
         sample_rows = list(range(rb, re, args.cpu_rows))
         c0 = time.perf_counter()
-        for r in sample_rows:
-            orc.trace(scene, w, full_h, rows=(r, r + 1), threads=threads)
+        orc.trace_rows(scene, w, full_h, sample_rows, threads=threads)
         c_s = time.perf_counter() - c0
         cpu = {"value": len(sample_rows) * w / c_s / 1e6, "unit": "Mrays/s", "cores": threads,
                "kind": "port",
                "sample": f"{len(sample_rows)} rows (every {args.cpu_rows}th of rank 0's band) x {w}"
-                         f" px of the same scene, oracle/rt_oracle.c orc_trace_mt, {c_s:.1f} s"}
+                         f" px of the same scene, oracle/rt_oracle.c orc_trace_rows_mt on "
+                         f"{threads} threads, {c_s:.1f} s"}
 
     if rank == 0:
         line = {

@@ -11,11 +11,13 @@
 //   prep   one lane per primitive: per-triangle fp64 constants, per-sphere
 //          fp32 constants, and a conservative integer pixel box outside of
 //          which the exact test provably rejects.
-//   bin    one lane per (64-primitive word, 32x32 bin): ordered candidate
-//          bitmasks, bit order = the reference's primitive order.
-//   trace  one 256-thread workgroup per bin, one 16x16 tile per wave, four
-//          pixels per lane; wave-uniform candidate loop on scalar loads,
-//          exact per-lane tests, 16-B coalesced framebuffer stores.
+//   coarse one wave per 64x64 coarse bin: ordered compact candidate list
+//          (ballot + mbcnt), order = the reference's primitive order.
+//   trace  one 256-thread workgroup per 32x32 bin: the coarse list (ids +
+//          boxes) staged in LDS once per workgroup, one 16x16 tile per wave
+//          filtered by ballot, four pixels per lane, wave-uniform candidate
+//          walk on scalar record loads, exact per-lane tests, 16-B coalesced
+//          framebuffer stores.
 // Plus `generic`, a brute-force per-pixel kernel for arbitrary ray origins
 // and directions (the reference's kernel arguments 8-9 in full generality).
 //
@@ -38,6 +40,8 @@ namespace {
 
 constexpr int kBinW = 32;         // bin = workgroup tile, pixels
 constexpr int kBinH = 32;
+constexpr int kCoarse = 64;       // coarse bin (candidate list) edge, pixels
+constexpr int kStage = 512;       // candidate entries staged in LDS per pass
 constexpr int kWaveTile = 16;     // each wave owns a 16x16 quadrant of the bin
 constexpr int kRowsPerLane = 4;   // lane rows y0, y0+4, y0+8, y0+12
 constexpr int kThreads = 256;
@@ -70,7 +74,11 @@ static_assert(sizeof(SphRec) == 32, "SphRec layout");
 
 struct Box { int x0, y0, x1, y1; };  // inclusive pixel range, empty if x0 > x1
 
-__host__ __device__ inline Box empty_box() { return Box{1, 1, 0, 0}; }
+// Inverted far-out-of-range box: fails every overlap test against any pixel
+// rectangle, so empty primitives can never reach a bin or a wave tile.
+__host__ __device__ inline Box empty_box() {
+    return Box{1 << 30, 1 << 30, -(1 << 30), -(1 << 30)};
+}
 
 __host__ __device__ inline bool finite3(double a, double b, double c) {
     return std::isfinite(a) && std::isfinite(b) && std::isfinite(c);
@@ -323,7 +331,7 @@ __global__ void __launch_bounds__(kThreads) generic_kernel(
 __global__ void __launch_bounds__(kThreads) prep_kernel(
     SceneDev scene, float4 dir, int width, int row_begin, int row_end,
     TriRec* __restrict__ tri, SphRec* __restrict__ sph, int4* __restrict__ boxes,
-    int* __restrict__ nonfinite_flag) {
+    unsigned* __restrict__ nonfinite_flag, unsigned gen) {
     const int n_tri = 12 * scene.n_cubes;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     Box b = empty_box();
@@ -348,54 +356,124 @@ __global__ void __launch_bounds__(kThreads) prep_kernel(
         return;
     }
     boxes[i] = make_int4(b.x0, b.y0, b.x1, b.y1);
-    if (bad) atomicOr(nonfinite_flag, 1);
+    if (bad) atomicMax(nonfinite_flag, gen);
 }
 
-// masks[w * n_bins + bin] bit j = primitive 64 w + j may touch bin `bin`.
-__global__ void __launch_bounds__(kThreads) bin_kernel(
-    const int4* __restrict__ boxes, int n_prims, int n_bins_x, int n_bins, int row_begin,
-    int n_words, unsigned long long* __restrict__ masks) {
-    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (gid >= (int64_t)n_words * n_bins) return;
-    const int w = (int)(gid / n_bins);
-    const int bin = (int)(gid % n_bins);
-    const int x0 = (bin % n_bins_x) * kBinW, x1 = x0 + kBinW - 1;
-    const int y0 = row_begin + (bin / n_bins_x) * kBinH, y1 = y0 + kBinH - 1;
-    unsigned long long m = 0;
-    const int base = w * 64;
-    const int lim = min(64, n_prims - base);
-    for (int j = 0; j < lim; ++j) {
-        const int4 b = boxes[base + j];
-        const bool hit = b.x <= x1 && b.z >= x0 && b.y <= y1 && b.w >= y0;
-        m |= (unsigned long long)hit << j;
+// Coarse binning: one wave per 64x64-pixel coarse bin writes the ordered
+// list of primitives whose box touches it (ballot + mbcnt compaction keeps
+// the reference's primitive order: cubes' triangles, then spheres).
+__global__ void __launch_bounds__(kThreads) coarse_kernel(
+    const int4* __restrict__ boxes, int n_prims, int n_cx, int n_coarse, int row_begin,
+    int cap, int* __restrict__ counts, int* __restrict__ lists) {
+    const int cb = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+    if (cb >= n_coarse) return;  // wave-uniform
+    const int lane = threadIdx.x & 63;
+    const int x0 = (cb % n_cx) * kCoarse, x1 = x0 + kCoarse - 1;
+    const int y0 = row_begin + (cb / n_cx) * kCoarse, y1 = y0 + kCoarse - 1;
+    int* out = lists + (int64_t)cb * cap;
+    int count = 0;
+    for (int base = 0; base < n_prims; base += 64) {
+        const int p = base + lane;
+        bool ov = false;
+        if (p < n_prims) {
+            const int4 b = boxes[p];
+            ov = b.x <= x1 && b.z >= x0 && b.y <= y1 && b.w >= y0;
+        }
+        const unsigned long long m = __ballot(ov);
+        if (ov) {
+            const unsigned below = __builtin_amdgcn_mbcnt_hi(
+                (unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+            out[count + (int)below] = p;
+        }
+        count += __popcll(m);
     }
-    masks[gid] = m;
+    if (lane == 0) counts[cb] = count;
 }
 
+// Per-lane exact tests of one candidate primitive `p` (wave-uniform) on the
+// lane's kRowsPerLane pixels.  Triangles: MainState.cpp:257-298 restated on
+// the per-triangle constants (see TriRec); spheres: :300-327 on SphRec.
+__device__ __forceinline__ void test_primitive(int p, int n_tri, const TriRec* __restrict__ tri,
+                                               const SphRec* __restrict__ sph, double px,
+                                               float pxf, const double* py, const float* pyf,
+                                               float* closest, int* hit) {
+    if (p < n_tri) {
+        const TriRec r = tri[p];
+        const double tx = px - r.v0x;
+#pragma unroll
+        for (int j = 0; j < kRowsPerLane; ++j) {
+            const double ty = py[j] - r.v0y;
+            // u = ((tx*p0 + ty*p1) + tz*p2) * inv_det, tz*p2 == +-0 for d = (0,0,D)
+            const double u = (tx * r.p0 + ty * r.p1) * r.inv_det;
+            // v = ((d0*q0 + d1*q1) + d2*q2) * inv_det, d0 = d1 = +-0
+            const double q2 = tx * r.e1y - ty * r.e1x;
+            const double v = (r.dz * q2) * r.inv_det;
+            const bool inside = !(u < 0.0 || u > 1.0) && !(v < 0.0 || u + v > 1.0);
+            if (inside) {
+                const double q0 = ty * r.e1z - r.k0;
+                const double q1 = r.k1 - tx * r.e1z;
+                const double t = (r.e2x * q0 + r.e2y * q1 + r.e2z * q2) * r.inv_det;
+                const float tf = (float)t;
+                if (tf < closest[j]) {
+                    closest[j] = tf;
+                    hit[j] = p;
+                }
+            }
+        }
+    } else {
+        const SphRec s = sph[p - n_tri];
+        const float lx = s.cx - pxf;
+        const float lx2 = lx * lx;
+#pragma unroll
+        for (int j = 0; j < kRowsPerLane; ++j) {
+            const float ly = s.cy - pyf[j];
+            const float a = lx2 + ly * ly;
+            const float dist2 = (a + s.kzw) - s.tca2;
+            if (!(dist2 > s.r2)) {
+                const float thc = sqrtf(s.r2 - dist2);
+                const float t0 = s.tca - thc;
+                if (t0 != 0.0f && t0 < closest[j]) {
+                    closest[j] = t0;
+                    hit[j] = p;
+                }
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ void store_pixel(void* __restrict__ out, int out_format, int64_t idx,
+                                            int4v pix) {
+    if (out_format == RT_FORMAT_I32X4)
+        reinterpret_cast<int4v*>(out)[idx] = pix;
+    else
+        reinterpret_cast<unsigned*>(out)[idx] = pack_rgba8(pix);
+}
+
+// One workgroup per 32x32 bin, one 16x16 tile per wave, kRowsPerLane pixels
+// per lane.  The parent coarse bin's candidate list (ids + boxes) is staged
+// in LDS once per workgroup; each wave filters it against its own tile with
+// one ballot per 64 entries and walks the surviving candidates in order
+// (v_readlane -> scalar record loads -> per-lane exact tests).
 __global__ void __launch_bounds__(kThreads) trace_kernel(
     SceneDev scene, const TriRec* __restrict__ tri, const SphRec* __restrict__ sph,
-    const int4* __restrict__ boxes, const unsigned long long* __restrict__ masks,
-    const int* __restrict__ nonfinite_flag, float4 dir, int width, int row_begin,
-    int row_end, int n_bins_x, int n_bins, int n_words, int out_format,
-    void* __restrict__ out) {
+    const int4* __restrict__ boxes, const int* __restrict__ counts,
+    const int* __restrict__ lists, int cap, const unsigned* __restrict__ nonfinite_flag,
+    unsigned gen, float4 dir, int width, int row_begin, int row_end, int n_bins_x, int n_cx,
+    int out_format, void* __restrict__ out) {
+    __shared__ int s_id[kStage];
+    __shared__ int4 s_box[kStage];
     const int bin = blockIdx.x;
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
-    const int tile_x = (bin % n_bins_x) * kBinW + (wave & 1) * kWaveTile;
-    const int tile_y = row_begin + (bin / n_bins_x) * kBinH + (wave >> 1) * kWaveTile;
+    const int bin_x = (bin % n_bins_x) * kBinW;
+    const int bin_y = (bin / n_bins_x) * kBinH;  // relative to row_begin
+    const int tile_x = bin_x + (wave & 1) * kWaveTile;
+    const int tile_y = row_begin + bin_y + (wave >> 1) * kWaveTile;
     const int x = tile_x + (lane & 15);
     const int y0 = tile_y + (lane >> 4);
     const int n_tri = 12 * scene.n_cubes;
 
-    float closest[kRowsPerLane];
-    int hit[kRowsPerLane];
-#pragma unroll
-    for (int j = 0; j < kRowsPerLane; ++j) {
-        closest[j] = kFar;
-        hit[j] = -1;
-    }
-
-    if (*nonfinite_flag) {
+    if (*nonfinite_flag == gen) {
         // Non-finite scene data: the algebraic shortcuts of the binned path
         // assume finite values, so run the reference algorithm verbatim.
 #pragma unroll 1
@@ -404,80 +482,59 @@ __global__ void __launch_bounds__(kThreads) trace_kernel(
             if (x >= width || y >= row_end) continue;
             const int4v p =
                 collide_generic(scene, make_float4((float)x, (float)y, 0.0f, 1.0f), dir);
-            const int64_t idx = (int64_t)(y - row_begin) * width + x;
-            if (out_format == RT_FORMAT_I32X4)
-                reinterpret_cast<int4v*>(out)[idx] = p;
-            else
-                reinterpret_cast<unsigned*>(out)[idx] = pack_rgba8(p);
+            store_pixel(out, out_format, (int64_t)(y - row_begin) * width + x, p);
         }
         return;
     }
 
-    const double px = (double)x;
-    const float pxf = (float)x;
+    float closest[kRowsPerLane];
+    int hit[kRowsPerLane];
     double py[kRowsPerLane];
     float pyf[kRowsPerLane];
 #pragma unroll
     for (int j = 0; j < kRowsPerLane; ++j) {
+        closest[j] = kFar;
+        hit[j] = -1;
         py[j] = (double)(y0 + 4 * j);
         pyf[j] = (float)(y0 + 4 * j);
     }
+    const double px = (double)x;
+    const float pxf = (float)x;
     const int tx1 = tile_x + kWaveTile - 1, ty1 = tile_y + kWaveTile - 1;
 
-    for (int w = 0; w < n_words; ++w) {
-        unsigned long long m = masks[(int64_t)w * n_bins + bin];
-        while (m) {
-            const int p = w * 64 + __builtin_ctzll(m);
-            m &= m - 1;
-            const int4 b = boxes[p];
-            if (b.x > tx1 || b.z < tile_x || b.y > ty1 || b.w < tile_y) continue;
-            if (p < n_tri) {
-                const TriRec r = tri[p];
-                const double tx = px - r.v0x;
-#pragma unroll
-                for (int j = 0; j < kRowsPerLane; ++j) {
-                    const double ty = py[j] - r.v0y;
-                    // u = ((tx*p0 + ty*p1) + tz*p2) * inv_det with tz*p2 == +-0
-                    const double u = (tx * r.p0 + ty * r.p1) * r.inv_det;
-                    // v = ((d0*q0 + d1*q1) + d2*q2) * inv_det with d0 = d1 = +-0
-                    const double q2 = tx * r.e1y - ty * r.e1x;
-                    const double v = (r.dz * q2) * r.inv_det;
-                    const bool inside = !(u < 0.0 || u > 1.0) && !(v < 0.0 || u + v > 1.0);
-                    if (inside) {
-                        const double q0 = ty * r.e1z - r.k0;
-                        const double q1 = r.k1 - tx * r.e1z;
-                        const double t = (r.e2x * q0 + r.e2y * q1 + r.e2z * q2) * r.inv_det;
-                        const float tf = (float)t;
-                        if (tf < closest[j]) {
-                            closest[j] = tf;
-                            hit[j] = p;
-                        }
-                    }
-                }
-            } else {
-                const SphRec s = sph[p - n_tri];
-                const float lx = s.cx - pxf;
-                const float lx2 = lx * lx;
-#pragma unroll
-                for (int j = 0; j < kRowsPerLane; ++j) {
-                    const float ly = s.cy - pyf[j];
-                    const float a = lx2 + ly * ly;
-                    const float dist2 = (a + s.kzw) - s.tca2;
-                    if (!(dist2 > s.r2)) {
-                        const float thc = sqrtf(s.r2 - dist2);
-                        const float t0 = s.tca - thc;
-                        if (t0 != 0.0f && t0 < closest[j]) {
-                            closest[j] = t0;
-                            hit[j] = p;
-                        }
-                    }
-                }
+    const int cb = (bin_y / kCoarse) * n_cx + bin_x / kCoarse;
+    const int count = counts[cb];
+    const int* __restrict__ list = lists + (int64_t)cb * cap;
+    for (int s0 = 0; s0 < count; s0 += kStage) {
+        const int n = min(kStage, count - s0);
+        if (s0 > 0) __syncthreads();  // previous stage fully consumed
+        for (int i = threadIdx.x; i < n; i += kThreads) {
+            const int id = list[s0 + i];
+            s_id[i] = id;
+            s_box[i] = boxes[id];
+        }
+        __syncthreads();
+        for (int c = 0; c < n; c += 64) {
+            const int e = c + lane;
+            bool ov = false;
+            int id = 0;
+            if (e < n) {
+                const int4 b = s_box[e];
+                id = s_id[e];
+                ov = b.x <= tx1 && b.z >= tile_x && b.y <= ty1 && b.w >= tile_y;
+            }
+            unsigned long long m = __ballot(ov);
+            while (m) {
+                const int bit = __builtin_ctzll(m);
+                m &= m - 1;
+                const int p = __builtin_amdgcn_readlane(id, bit);
+                test_primitive(p, n_tri, tri, sph, px, pxf, py, pyf, closest, hit);
             }
         }
     }
 
-    // Shade + store.  Waves with no hit at all store the black pattern
-    // without touching the colour arrays.
+    // Shade + store.  A wave whose 256 pixels all missed (ballot) stores the
+    // black pattern without touching the colour arrays.
     const bool any_hit =
         __ballot(hit[0] >= 0 || hit[1] >= 0 || hit[2] >= 0 || hit[3] >= 0) != 0ull;
 #pragma unroll
@@ -489,13 +546,7 @@ __global__ void __launch_bounds__(kThreads) trace_kernel(
                                               : scene.sphere_colours[hit[j] - n_tri];
             pix = shade(closest[j], col);
         }
-        if (x < width && y < row_end) {
-            const int64_t idx = (int64_t)(y - row_begin) * width + x;
-            if (out_format == RT_FORMAT_I32X4)
-                reinterpret_cast<int4v*>(out)[idx] = pix;
-            else
-                reinterpret_cast<unsigned*>(out)[idx] = pack_rgba8(pix);
-        }
+        if (x < width && y < row_end) store_pixel(out, out_format, (int64_t)(y - row_begin) * width + x, pix);
     }
 }
 
@@ -520,11 +571,13 @@ struct rt_ctx {
     void* origin_buf = nullptr; size_t origin_cap = 0;  // host-API explicit origins
     void* out_buf = nullptr;    size_t out_cap = 0;     // host-API frame
     void* rec_buf = nullptr;    size_t rec_cap = 0;     // TriRec/SphRec/boxes/flag
-    void* mask_buf = nullptr;   size_t mask_cap = 0;    // bin masks
+    void* list_buf = nullptr;   size_t list_cap = 0;    // coarse-bin candidate lists
+    unsigned* flag = nullptr;   // non-finite scene flag (generation-stamped)
+    unsigned gen = 0;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     // profiling
     bool profile = false;
-    std::vector<hipEvent_t> prof_events;  // quads: start, prep, bin, trace
+    std::vector<hipEvent_t> prof_events;  // quads: start, prep, coarse, trace
     int32_t prof_count = 0;
 };
 
@@ -615,47 +668,52 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
     }
     const int n_tri = 12 * s->num_cubes;
     const int n_prims = n_tri + s->num_spheres;
-    const int n_words = (n_prims + 63) / 64;
     const int n_bins_x = (width + kBinW - 1) / kBinW;
     const int n_bins_y = (rows + kBinH - 1) / kBinH;
+    const int n_cx = (width + kCoarse - 1) / kCoarse;
+    const int n_cy = (rows + kCoarse - 1) / kCoarse;
     const int64_t n_bins64 = (int64_t)n_bins_x * n_bins_y;
-    if (n_bins64 > (int64_t)1 << 31) return RT_ERR_INVALID_ARG;
+    const int64_t n_coarse64 = (int64_t)n_cx * n_cy;
+    if (n_bins64 >= (int64_t)1 << 31) return RT_ERR_INVALID_ARG;
     const int n_bins = (int)n_bins64;
+    const int n_coarse = (int)n_coarse64;
+    const int cap = n_prims > 0 ? n_prims : 1;
 
     const size_t tri_off = 0;
     const size_t sph_off = align_up(sizeof(TriRec) * (size_t)n_tri, 256);
     const size_t box_off = sph_off + align_up(sizeof(SphRec) * (size_t)s->num_spheres, 256);
-    const size_t flag_off = box_off + align_up(sizeof(int4) * (size_t)n_prims, 256);
-    const size_t rec_need = flag_off + 256;
+    const size_t cnt_off = box_off + align_up(sizeof(int4) * (size_t)n_prims, 256);
+    const size_t rec_need = cnt_off + align_up(sizeof(int) * (size_t)n_coarse, 256);
     int rc = ensure(&ctx->rec_buf, &ctx->rec_cap, rec_need);
     if (rc) return rc;
-    const size_t mask_need = sizeof(unsigned long long) * (size_t)n_words * (size_t)n_bins + 256;
-    rc = ensure(&ctx->mask_buf, &ctx->mask_cap, mask_need);
+    const size_t list_need = sizeof(int) * (size_t)cap * (size_t)n_coarse + 256;
+    rc = ensure(&ctx->list_buf, &ctx->list_cap, list_need);
     if (rc) return rc;
     char* base = static_cast<char*>(ctx->rec_buf);
     TriRec* tri = reinterpret_cast<TriRec*>(base + tri_off);
     SphRec* sph = reinterpret_cast<SphRec*>(base + sph_off);
     int4* boxes = reinterpret_cast<int4*>(base + box_off);
-    int* flag = reinterpret_cast<int*>(base + flag_off);
-    auto* masks = static_cast<unsigned long long*>(ctx->mask_buf);
+    int* counts = reinterpret_cast<int*>(base + cnt_off);
+    int* lists = static_cast<int*>(ctx->list_buf);
+    // generation-stamped non-finite flag: no per-launch memset needed
+    if (++ctx->gen == 0) {
+        HIP_TRY(hipMemsetAsync(ctx->flag, 0, sizeof(unsigned), stream));
+        ctx->gen = 1;
+    }
 
-    HIP_TRY(hipMemsetAsync(flag, 0, sizeof(int), stream));
     if (n_prims > 0) {
         prep_kernel<<<dim3((n_prims + kThreads - 1) / kThreads), dim3(kThreads), 0, stream>>>(
-            sd, dir, width, row_begin, row_end, tri, sph, boxes, flag);
+            sd, dir, width, row_begin, row_end, tri, sph, boxes, ctx->flag, ctx->gen);
         HIP_TRY(hipGetLastError());
     }
     if (pe) HIP_TRY(hipEventRecord(pe[1], stream));
-    if (n_words > 0) {
-        const int64_t n = (int64_t)n_words * n_bins;
-        bin_kernel<<<dim3((unsigned)((n + kThreads - 1) / kThreads)), dim3(kThreads), 0,
-                     stream>>>(boxes, n_prims, n_bins_x, n_bins, row_begin, n_words, masks);
-        HIP_TRY(hipGetLastError());
-    }
+    coarse_kernel<<<dim3((n_coarse + 3) / 4), dim3(kThreads), 0, stream>>>(
+        boxes, n_prims, n_cx, n_coarse, row_begin, cap, counts, lists);
+    HIP_TRY(hipGetLastError());
     if (pe) HIP_TRY(hipEventRecord(pe[2], stream));
     trace_kernel<<<dim3((unsigned)n_bins), dim3(kThreads), 0, stream>>>(
-        sd, tri, sph, boxes, masks, flag, dir, width, row_begin, row_end, n_bins_x, n_bins,
-        n_words, fmt, out);
+        sd, tri, sph, boxes, counts, lists, cap, ctx->flag, ctx->gen, dir, width, row_begin,
+        row_end, n_bins_x, n_cx, fmt, out);
     HIP_TRY(hipGetLastError());
     if (pe) HIP_TRY(hipEventRecord(pe[3], stream));
     return RT_OK;
@@ -696,6 +754,11 @@ int rt_init(int device_ordinal, rt_ctx** out_ctx) {
             return RT_ERR_HIP;
         }
     }
+    if (hipMalloc(&ctx->flag, sizeof(unsigned)) != hipSuccess ||
+        hipMemset(ctx->flag, 0, sizeof(unsigned)) != hipSuccess) {
+        rt_destroy(ctx);
+        return RT_ERR_OUT_OF_MEMORY;
+    }
     *out_ctx = ctx;
     return RT_OK;
 }
@@ -704,7 +767,8 @@ void rt_destroy(rt_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-    for (void* p : {ctx->scene_buf, ctx->origin_buf, ctx->out_buf, ctx->rec_buf, ctx->mask_buf})
+    for (void* p : {ctx->scene_buf, ctx->origin_buf, ctx->out_buf, ctx->rec_buf, ctx->list_buf,
+                    static_cast<void*>(ctx->flag)})
         if (p) (void)hipFree(p);
     for (auto& e : ctx->ev)
         if (e) (void)hipEventDestroy(e);

@@ -575,6 +575,44 @@ void orc_trace_mt(int32_t width, int32_t height, int32_t row_begin, int32_t row_
     for (int i = 0; i < n_threads; ++i) pthread_join(th[i], NULL);
 }
 
+typedef struct {
+    int32_t width, height, n_rows, stride, phase;
+    const int32_t* rows;
+    const float *ray_dir, *ray_origins;
+    int32_t n_spheres, n_cubes;
+    const float *so, *sr, *sc, *cv, *cc;
+    int32_t* out;
+} rows_job;
+
+static void* rows_worker(void* arg) {
+    rows_job* j = (rows_job*)arg;
+    for (int32_t i = j->phase; i < j->n_rows; i += j->stride)
+        orc_trace(j->width, j->height, j->rows[i], j->rows[i] + 1, j->ray_dir, j->ray_origins,
+                  j->n_spheres, j->so, j->sr, j->sc, j->n_cubes, j->cv, j->cc,
+                  j->out + 4 * (int64_t)i * j->width);
+    return NULL;
+}
+
+void orc_trace_rows_mt(int32_t width, int32_t height, const int32_t* rows, int32_t n_rows,
+                       const float ray_dir[4], const float* ray_origins, int32_t n_spheres,
+                       const float* sphere_origins, const float* sphere_radius,
+                       const float* sphere_colours, int32_t n_cubes,
+                       const float* cube_vertices, const float* cube_colours, int32_t* out,
+                       int32_t n_threads) {
+    if (n_threads < 1) n_threads = 1;
+    if (n_threads > 256) n_threads = 256;
+    pthread_t th[256];
+    rows_job jobs[256];
+    for (int i = 0; i < n_threads; ++i) {
+        rows_job j = {width, height, n_rows, n_threads, i, rows, ray_dir, ray_origins,
+                      n_spheres, n_cubes, sphere_origins, sphere_radius, sphere_colours,
+                      cube_vertices, cube_colours, out};
+        jobs[i] = j;
+        pthread_create(&th[i], NULL, rows_worker, &jobs[i]);
+    }
+    for (int i = 0; i < n_threads; ++i) pthread_join(th[i], NULL);
+}
+
 uint64_t orc_fnv1a_i32(const int32_t* v, int64_t n) {
     uint64_t h = 0xcbf29ce484222325ull;
     for (int64_t i = 0; i < n; ++i) {

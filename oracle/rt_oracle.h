@@ -86,6 +86,16 @@ void orc_trace_mt(int32_t width, int32_t height, int32_t row_begin,
                   const float* cube_vertices, const float* cube_colours,
                   int32_t* out, int32_t n_threads);
 
+/* The listed rows (any order), each into out[i] (n_rows x W x 4), over
+ * `n_threads` threads: the CPU-baseline row sample. */
+void orc_trace_rows_mt(int32_t width, int32_t height, const int32_t* rows,
+                       int32_t n_rows, const float ray_dir[4],
+                       const float* ray_origins, int32_t n_spheres,
+                       const float* sphere_origins, const float* sphere_radius,
+                       const float* sphere_colours, int32_t n_cubes,
+                       const float* cube_vertices, const float* cube_colours,
+                       int32_t* out, int32_t n_threads);
+
 /* The reference's fp32 OpenCL kernel semantics (rayTracer.cl:37-202), for
  * the SURVEY.md F5 divergence pin only -- not the parity target. */
 void orc_trace_cl32(int32_t width, int32_t height, const float ray_dir[4],

@@ -48,6 +48,8 @@ def _load() -> ctypes.CDLL:
                              _vp, _vp]),
         "orc_trace_mt": (None, [_i32, _i32, _i32, _i32, _vp, _vp, _i32, _vp, _vp, _vp, _i32, _vp,
                                 _vp, _vp, _i32]),
+        "orc_trace_rows_mt": (None, [_i32, _i32, _vp, _i32, _vp, _vp, _i32, _vp, _vp, _vp, _i32,
+                                     _vp, _vp, _vp, _i32]),
         "orc_trace_cl32": (None, [_i32, _i32, _vp, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _vp]),
         "orc_fnv1a_i32": (ctypes.c_uint64, [_vp, ctypes.c_int64]),
         "orc_pack_rgba8": (None, [_vp, ctypes.c_int64, _vp]),
@@ -121,6 +123,17 @@ class Oracle:
         else:
             self.lib.orc_trace(width, height, rb, re, _p(d), _p(org), len(sr), _p(so), _p(sr),
                                _p(sc), len(cc), _p(cv), _p(cc), _p(out))
+        return out
+
+    def trace_rows(self, scene, width: int, height: int, rows, threads: int = 1,
+                   ray_dir: Optional[np.ndarray] = None) -> np.ndarray:
+        """Render the listed rows (one output row each), multi-threaded."""
+        so, sr, sc, cv, cc = self._arrays(scene)
+        d = self.ray_dir() if ray_dir is None else np.ascontiguousarray(ray_dir, np.float32)
+        r = np.ascontiguousarray(rows, np.int32)
+        out = np.zeros((len(r), width, 4), np.int32)
+        self.lib.orc_trace_rows_mt(width, height, _p(r), len(r), _p(d), None, len(sr), _p(so),
+                                   _p(sr), _p(sc), len(cc), _p(cv), _p(cc), _p(out), threads)
         return out
 
     def trace_cl32(self, scene, width: int, height: int) -> np.ndarray:

@@ -240,3 +240,14 @@ def test_device_api_into_torch(pkg, rt):
     rt.render_device(ds, 640, 480, (0, 480), out.data_ptr(), stream=stream)
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy(), g["frame"])
+
+
+def test_candidate_lists_larger_than_lds_stage(pkg, rt, oracle):
+    """> kStage (512) candidates in one 64x64 coarse bin: the trace kernel
+    stages the list through LDS in several passes, order preserved."""
+    w, h = 100, 90
+    scene = pkg.Scene.synthetic(w, h, 700, 40, seed=11, k=0.4)
+    got, t = rt.render(scene, w, h)
+    assert t.path == "binned"
+    want = oracle.trace(scene, w, h, threads=THREADS)
+    assert not diff_report(got, want), diff_report(got, want)
