@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--trace-mode", type=int, default=0,
+                    help="diagnostics ablation: 1 = stores only, 2 = no per-pixel tests")
     ap.add_argument("--pmc", default=str(REPO / "profiles" / "r01_pmc_config3.json"),
                     help="committed PMC summary to read `traffic` from")
     return ap.parse_args()
@@ -86,6 +88,7 @@ def main():
     rb, re = rank * rows, (rank + 1) * rows
 
     rt = pkg.RayTracer(local)
+    rt.set_trace_mode(args.trace_mode)
     t = {name: torch.from_numpy(np.ascontiguousarray(getattr(scene, name))).to(dev)
          for name in ("sphere_origins", "sphere_radius", "sphere_colours", "cube_vertices",
                       "cube_colours")}

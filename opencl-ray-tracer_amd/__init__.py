@@ -84,6 +84,15 @@ def library() -> ctypes.CDLL:
     path = library_path()
     if not path.exists():
         raise RuntimeError(f"{path} is missing: build it with `make -C {PKG_DIR / 'csrc'}`")
+    # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64.so.7
+    # (same SONAME as /opt/rocm's).  Whichever is loaded first serves every
+    # later user, and torch cannot run on a runtime other than its own, so
+    # load torch's first when torch is installed (RT_NO_TORCH=1 opts out).
+    if os.environ.get("RT_NO_TORCH", "0") != "1":
+        try:
+            import torch  # noqa: F401  (plumbing: device memory, streams, RCCL)
+        except ImportError:
+            pass
     lib = ctypes.CDLL(str(path))
     vp, i32, f32 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_float
     sig = {
@@ -118,6 +127,7 @@ def library() -> ctypes.CDLL:
         "rt_selftest_fp32": (ctypes.c_int, [vp, vp, i32, vp, vp]),
         "rt_debug_triangle_box": (ctypes.c_int, [vp, vp, vp, vp, i32, i32, i32, vp]),
         "rt_debug_sphere_box": (ctypes.c_int, [vp, f32, vp, i32, i32, i32, vp]),
+        "rt_debug_set_trace_mode": (ctypes.c_int, [vp, ctypes.c_int]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -331,6 +341,10 @@ class RayTracer:
         _check(library().rt_profile_read(self._ctx, ctypes.byref(a), ctypes.byref(b),
                                          ctypes.byref(c), ctypes.byref(n)), "rt_profile_read")
         return {"prep_ms": a.value, "bin_ms": b.value, "trace_ms": c.value, "renders": n.value}
+
+    def set_trace_mode(self, mode: int) -> None:
+        """Diagnostics ablation of the trace kernel (0 = normal)."""
+        _check(library().rt_debug_set_trace_mode(self._ctx, mode), "rt_debug_set_trace_mode")
 
     def device_info(self) -> dict:
         name = ctypes.create_string_buffer(256)

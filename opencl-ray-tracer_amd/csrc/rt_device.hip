@@ -454,6 +454,10 @@ __device__ __forceinline__ void store_pixel(void* __restrict__ out, int out_form
 // in LDS once per workgroup; each wave filters it against its own tile with
 // one ballot per 64 entries and walks the surviving candidates in order
 // (v_readlane -> scalar record loads -> per-lane exact tests).
+// kMode is a diagnostics ablation (rt_debug_set_trace_mode): 0 = the real
+// kernel, 1 = stores only (the store floor of this exact pattern), 2 = stage
+// and filter candidates but skip the per-pixel tests.
+template <int kMode>
 __global__ void __launch_bounds__(kThreads) trace_kernel(
     SceneDev scene, const TriRec* __restrict__ tri, const SphRec* __restrict__ sph,
     const int4* __restrict__ boxes, const int* __restrict__ counts,
@@ -473,7 +477,7 @@ __global__ void __launch_bounds__(kThreads) trace_kernel(
     const int y0 = tile_y + (lane >> 4);
     const int n_tri = 12 * scene.n_cubes;
 
-    if (*nonfinite_flag == gen) {
+    if (kMode == 0 && *nonfinite_flag == gen) {
         // Non-finite scene data: the algebraic shortcuts of the binned path
         // assume finite values, so run the reference algorithm verbatim.
 #pragma unroll 1
@@ -503,7 +507,7 @@ __global__ void __launch_bounds__(kThreads) trace_kernel(
     const int tx1 = tile_x + kWaveTile - 1, ty1 = tile_y + kWaveTile - 1;
 
     const int cb = (bin_y / kCoarse) * n_cx + bin_x / kCoarse;
-    const int count = counts[cb];
+    const int count = kMode == 1 ? 0 : counts[cb];
     const int* __restrict__ list = lists + (int64_t)cb * cap;
     for (int s0 = 0; s0 < count; s0 += kStage) {
         const int n = min(kStage, count - s0);
@@ -528,6 +532,10 @@ __global__ void __launch_bounds__(kThreads) trace_kernel(
                 const int bit = __builtin_ctzll(m);
                 m &= m - 1;
                 const int p = __builtin_amdgcn_readlane(id, bit);
+                if (kMode == 2) {
+                    hit[0] = hit[0] > p ? hit[0] : -1;  // keep the walk alive
+                    continue;
+                }
                 test_primitive(p, n_tri, tri, sph, px, pxf, py, pyf, closest, hit);
             }
         }
@@ -574,6 +582,7 @@ struct rt_ctx {
     void* list_buf = nullptr;   size_t list_cap = 0;    // coarse-bin candidate lists
     unsigned* flag = nullptr;   // non-finite scene flag (generation-stamped)
     unsigned gen = 0;
+    int trace_mode = 0;  // diagnostics ablation, see trace_kernel
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     // profiling
     bool profile = false;
@@ -711,7 +720,9 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
         boxes, n_prims, n_cx, n_coarse, row_begin, cap, counts, lists);
     HIP_TRY(hipGetLastError());
     if (pe) HIP_TRY(hipEventRecord(pe[2], stream));
-    trace_kernel<<<dim3((unsigned)n_bins), dim3(kThreads), 0, stream>>>(
+    auto kern = ctx->trace_mode == 1 ? trace_kernel<1>
+              : ctx->trace_mode == 2 ? trace_kernel<2> : trace_kernel<0>;
+    kern<<<dim3((unsigned)n_bins), dim3(kThreads), 0, stream>>>(
         sd, tri, sph, boxes, counts, lists, cap, ctx->flag, ctx->gen, dir, width, row_begin,
         row_end, n_bins_x, n_cx, fmt, out);
     HIP_TRY(hipGetLastError());
@@ -941,6 +952,13 @@ int rt_debug_triangle_box(const float v0[3], const float v1[3], const float v2[3
                                   &r, &b, &bad);
     box_out[0] = b.x0; box_out[1] = b.y0; box_out[2] = b.x1; box_out[3] = b.y1;
     return ok ? 1 : 0;
+}
+
+// Diagnostics: select a trace-kernel ablation (0 = normal).
+int rt_debug_set_trace_mode(rt_ctx* ctx, int mode) {
+    if (!ctx || mode < 0 || mode > 2) return RT_ERR_INVALID_ARG;
+    ctx->trace_mode = mode;
+    return RT_OK;
 }
 
 int rt_debug_sphere_box(const float origin[4], float radius, const float dir[4], int32_t width,
