@@ -162,21 +162,24 @@ def main():
 
     gather = None
     if distributed and not args.no_gather:
-        gl = [torch.empty_like(out) for _ in range(world)] if rank == 0 else None
+        # Texture assembly on rank 0 (north_star): one RCCL gather of the bands.
+        from opencl_ray_tracer_amd import rowbands
+
         for _ in range(2):
-            dist.gather(out, gl, dst=0)
+            rowbands.gather_frame(out, full_h, world, rank)
         torch.cuda.synchronize(dev)
         barrier()
         g0 = time.perf_counter()
         reps = max(3, args.steps // 4)
         for _ in range(reps):
-            dist.gather(out, gl, dst=0)
+            rowbands.gather_frame(out, full_h, world, rank)
         torch.cuda.synchronize(dev)
         barrier()
         g_ms = (time.perf_counter() - g0) * 1e3 / reps
-        gather = {"collective": "rccl gather to rank 0", "ms": g_ms,
+        gather = {"collective": "rccl gather of row bands to rank 0", "ms": round(g_ms, 4),
                   "bytes_to_root": algo_bytes * (world - 1),
-                  "render_plus_gather_mrays": world * rays_rank / ((wall_ms + g_ms) * 1e-3) / 1e6}
+                  "render_plus_gather_mrays": round(
+                      world * rays_rank / ((wall_ms + g_ms) * 1e-3) / 1e6, 1)}
 
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:

@@ -20,7 +20,8 @@ from typing import Optional, Tuple
 import numpy as np
 
 __all__ = [
-    "RT_OK", "RT_FORMAT_I32X4", "RT_FORMAT_RGBA8", "RT_PATH_AUTO", "RT_PATH_BINNED",
+    "RT_OK", "RT_ERR_INVALID_ARG", "RT_ERR_NO_DEVICE", "RT_ERR_HIP", "RT_ERR_OUT_OF_MEMORY",
+    "RT_ERR_UNSUPPORTED", "RT_FORMAT_I32X4", "RT_FORMAT_RGBA8", "RT_PATH_AUTO", "RT_PATH_BINNED",
     "RT_PATH_GENERIC", "RtError", "Scene", "Timing", "RayTracer", "MainState",
     "library", "library_path", "primary_ray_dir", "pack_rgba8", "cube_packed",
     "deg_to_rad", "EXPORTED_SYMBOLS",
@@ -28,6 +29,8 @@ __all__ = [
 
 PKG_DIR = Path(__file__).resolve().parent
 RT_OK = 0
+RT_ERR_INVALID_ARG, RT_ERR_NO_DEVICE, RT_ERR_HIP = -1, -2, -3
+RT_ERR_OUT_OF_MEMORY, RT_ERR_UNSUPPORTED = -4, -5
 RT_FORMAT_I32X4, RT_FORMAT_RGBA8 = 0, 1
 RT_PATH_AUTO, RT_PATH_BINNED, RT_PATH_GENERIC = 0, 1, 2
 _FORMATS = {"i32x4": RT_FORMAT_I32X4, "rgba8": RT_FORMAT_RGBA8}
@@ -125,8 +128,8 @@ def library() -> ctypes.CDLL:
         "rt_pack_rgba8": (None, [vp, ctypes.c_int64, vp]),
         "rt_abi_version": (ctypes.c_int, []),
         "rt_selftest_fp32": (ctypes.c_int, [vp, vp, i32, vp, vp]),
-        "rt_debug_triangle_box": (ctypes.c_int, [vp, vp, vp, vp, i32, i32, i32, vp]),
-        "rt_debug_sphere_box": (ctypes.c_int, [vp, f32, vp, i32, i32, i32, vp]),
+        "rt_debug_triangle_box": (ctypes.c_int, [vp, vp, vp, vp, i32, i32, i32, vp, vp]),
+        "rt_debug_sphere_box": (ctypes.c_int, [vp, f32, vp, i32, i32, i32, vp, vp]),
         "rt_debug_set_trace_mode": (ctypes.c_int, [vp, ctypes.c_int]),
     }
     for name, (res, args) in sig.items():
@@ -359,6 +362,29 @@ class RayTracer:
         _check(library().rt_selftest_fp32(self._ctx, _ptr(x), x.size, _ptr(s), _ptr(q)),
                "rt_selftest_fp32")
         return s, q
+
+
+def debug_triangle_prep(v0, v1, v2, ray_dir, width, row_begin, row_end):
+    """Host evaluation of the prep kernel's triangle box and tile classifier
+    (the same __host__ __device__ code).  Returns (valid, box[4], cls[8])."""
+    a = [np.ascontiguousarray(v, np.float32)[:3].copy() for v in (v0, v1, v2)]
+    d = np.ascontiguousarray(ray_dir, np.float32)
+    box = np.zeros(4, np.int32)
+    cls = np.zeros(8, np.float32)
+    ok = library().rt_debug_triangle_box(_ptr(a[0]), _ptr(a[1]), _ptr(a[2]), _ptr(d), width,
+                                         row_begin, row_end, _ptr(box), _ptr(cls))
+    return bool(ok), box, cls
+
+
+def debug_sphere_prep(origin, radius, ray_dir, width, row_begin, row_end):
+    """Host evaluation of the prep kernel's sphere box and classifier."""
+    o = np.ascontiguousarray(origin, np.float32)
+    d = np.ascontiguousarray(ray_dir, np.float32)
+    box = np.zeros(4, np.int32)
+    cls = np.zeros(8, np.float32)
+    ok = library().rt_debug_sphere_box(_ptr(o), float(radius), _ptr(d), width, row_begin,
+                                       row_end, _ptr(box), _ptr(cls))
+    return bool(ok), box, cls
 
 
 class MainState:

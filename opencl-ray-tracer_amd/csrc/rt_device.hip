@@ -41,7 +41,7 @@ namespace {
 constexpr int kBinW = 32;         // bin = workgroup tile, pixels
 constexpr int kBinH = 32;
 constexpr int kCoarse = 64;       // coarse bin (candidate list) edge, pixels
-constexpr int kStage = 512;       // candidate entries staged in LDS per pass
+constexpr int kStage = 256;       // candidate entries staged in LDS per pass
 constexpr int kWaveTile = 16;     // each wave owns a 16x16 quadrant of the bin
 constexpr int kRowsPerLane = 4;   // lane rows y0, y0+4, y0+8, y0+12
 constexpr int kThreads = 256;
@@ -71,6 +71,18 @@ struct alignas(16) SphRec {
     float r2, tca, pad0, pad1;
 };
 static_assert(sizeof(SphRec) == 32, "SphRec layout");
+
+// Per-primitive tile classifier (32 B, fp32, staged in LDS with the box).
+// Triangle: a = (v0x, v0y, au, bu), b = (av, bv, g, 0) with the exact
+// barycentrics u = au (x - v0x) + bu (y - v0y), v = av (x - v0x) + bv (y -
+// v0y) up to a margin g that also covers the fp64 rounding of the per-pixel
+// test, so a 16x16 tile can be proven fully outside (skip) or fully inside
+// (no u/v tests, t only) in fp32.  g = +inf disables both.
+// Sphere: a = (cx, cy, R2, 0): every pixel farther than sqrt(R2) misses.
+struct Cls {
+    float4 a, b;
+};
+static_assert(sizeof(Cls) == 32, "Cls layout");
 
 struct Box { int x0, y0, x1, y1; };  // inclusive pixel range, empty if x0 > x1
 
@@ -105,7 +117,7 @@ __host__ __device__ inline int clamp_ceil(double v, int lo, int hi) {
 __host__ __device__ inline bool prep_triangle(const float* a, const float* b, const float* c,
                                               double dx, double dy, double dz, int width,
                                               int row_begin, int row_end, TriRec* rec,
-                                              Box* box, bool* nonfinite) {
+                                              Box* box, Cls* cls, bool* nonfinite) {
     const double v0[3] = {a[0], a[1], a[2]};
     const double v1[3] = {b[0], b[1], b[2]};
     const double v2[3] = {c[0], c[1], c[2]};
@@ -118,6 +130,8 @@ __host__ __device__ inline bool prep_triangle(const float* a, const float* b, co
     const double p2 = dx * e2[1] - dy * e2[0];
     const double det = e1[0] * p0 + e1[1] * p1 + e1[2] * p2;
     *box = empty_box();
+    cls->a = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    cls->b = make_float4(0.0f, 0.0f, INFINITY, 0.0f);
     if ((det > -kEpsilon && det < kEpsilon) || !(det == det) || *nonfinite) return false;
     const double inv_det = 1.0 / det;
     const double tz = 0.0 - v0[2];
@@ -140,9 +154,10 @@ __host__ __device__ inline bool prep_triangle(const float* a, const float* b, co
     const double eps = 1.1102230246251565e-16;  // 2^-53
     const double mnx = fmin(v0[0], fmin(v1[0], v2[0])), mxx = fmax(v0[0], fmax(v1[0], v2[0]));
     const double mny = fmin(v0[1], fmin(v1[1], v2[1])), mxy = fmax(v0[1], fmax(v1[1], v2[1]));
-    const double tx_max = fmax(fabs(0.0 - v0[0]), fabs((double)(width - 1) - v0[0])) + 1.0;
+    // |tx|, |ty| bounds over the band, widened by one bin for tile overhang
+    const double tx_max = fmax(fabs(0.0 - v0[0]), fabs((double)(width + 31) - v0[0])) + 1.0;
     const double ty_max =
-        fmax(fabs((double)row_begin - v0[1]), fabs((double)(row_end - 1) - v0[1])) + 1.0;
+        fmax(fabs((double)row_begin - v0[1]), fabs((double)(row_end + 31) - v0[1])) + 1.0;
     const double adet = fabs(det);
     const double rho =
         8.0 * eps * (fabs(e1[0] * p0) + fabs(e1[1] * p1) + fabs(e1[2] * p2)) / adet + 4.0 * eps;
@@ -152,6 +167,14 @@ __host__ __device__ inline bool prep_triangle(const float* a, const float* b, co
                           ty_max * (fabs(p1) + fabs(e1[0] * dz))) * fabs(inv_det);
         const double err = (32.0 * eps + 4.0 * rho) * s + 32.0 * eps;
         const double g = 2.0 * err + 8.0 * eps * s + 32.0 * eps;
+        // fp32 tile-classifier planes and their margin (fp32 rounding of the
+        // coefficients and of the corner evaluation, 2^-24 each, x32 slack)
+        const double au = p0 * inv_det, bu = p1 * inv_det;
+        const double av = dz * e1[1] * inv_det, bv = -(dz * e1[0]) * inv_det;
+        const double suv = (fabs(au) + fabs(av)) * tx_max + (fabs(bu) + fabs(bv)) * ty_max;
+        const double gm = g + 32.0 * 5.9604644775390625e-08 * suv + 1e-6;
+        cls->a = make_float4((float)v0[0], (float)v0[1], (float)au, (float)bu);
+        cls->b = make_float4((float)av, (float)bv, (float)(gm * (1.0 + 1e-6)), 0.0f);
         const double padx = 8.0 * (mxx - mnx) * g + 0.5;
         const double pady = 8.0 * (mxy - mny) * g + 0.5;
         bx.x0 = clamp_floor(mnx - padx, 0, width - 1);
@@ -173,9 +196,11 @@ __host__ __device__ inline bool prep_triangle(const float* a, const float* b, co
 // and the two sums); the box is that radius plus one pixel.
 __host__ __device__ inline void prep_sphere(const float* o, float radius, float dx, float dy,
                                             float dz, float dw, int width, int row_begin,
-                                            int row_end, SphRec* rec, Box* box,
+                                            int row_end, SphRec* rec, Box* box, Cls* cls,
                                             bool* nonfinite) {
     *box = empty_box();
+    cls->a = make_float4(o[0], o[1], -1.0f, 0.0f);
+    cls->b = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
     *nonfinite = !(std::isfinite(o[0]) && std::isfinite(o[1]) && std::isfinite(o[2]) &&
                    std::isfinite(o[3]) && std::isfinite(radius));
     const float lz = o[2] - 0.0f;
@@ -200,6 +225,7 @@ __host__ __device__ inline void prep_sphere(const float* o, float radius, float 
                          (1.0 - 8.0 * e);
     if (!(bound >= 0.0)) return;  // every pixel misses
     const double r = sqrt(bound * (1.0 + 1e-6) + 1e-6) + 1.0;
+    cls->a.z = (float)(bound * (1.0 + 1e-5) + 1e-5);
     const double cx = o[0], cy = o[1];
     if (cx + r < 0.0 || cx - r > (double)(width - 1) || cy + r < (double)row_begin ||
         cy - r > (double)(row_end - 1))
@@ -331,10 +357,11 @@ __global__ void __launch_bounds__(kThreads) generic_kernel(
 __global__ void __launch_bounds__(kThreads) prep_kernel(
     SceneDev scene, float4 dir, int width, int row_begin, int row_end,
     TriRec* __restrict__ tri, SphRec* __restrict__ sph, int4* __restrict__ boxes,
-    unsigned* __restrict__ nonfinite_flag, unsigned gen) {
+    Cls* __restrict__ cls, unsigned* __restrict__ nonfinite_flag, unsigned gen) {
     const int n_tri = 12 * scene.n_cubes;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     Box b = empty_box();
+    Cls k{};
     bool bad = false;
     if (i < n_tri) {
         const float4* v = scene.cube_vertices + 3 * i;
@@ -342,7 +369,7 @@ __global__ void __launch_bounds__(kThreads) prep_kernel(
         const float fa[3] = {a.x, a.y, a.z}, fb[3] = {bb.x, bb.y, bb.z}, fc[3] = {c.x, c.y, c.z};
         TriRec r{};
         prep_triangle(fa, fb, fc, (double)dir.x, (double)dir.y, (double)dir.z, width, row_begin,
-                      row_end, &r, &b, &bad);
+                      row_end, &r, &b, &k, &bad);
         tri[i] = r;
     } else if (i < n_tri + scene.n_spheres) {
         const int s = i - n_tri;
@@ -350,12 +377,13 @@ __global__ void __launch_bounds__(kThreads) prep_kernel(
         const float fo[4] = {o.x, o.y, o.z, o.w};
         SphRec r{};
         prep_sphere(fo, scene.sphere_radius[s], dir.x, dir.y, dir.z, dir.w, width, row_begin,
-                    row_end, &r, &b, &bad);
+                    row_end, &r, &b, &k, &bad);
         sph[s] = r;
     } else {
         return;
     }
     boxes[i] = make_int4(b.x0, b.y0, b.x1, b.y1);
+    cls[i] = k;
     if (bad) atomicMax(nonfinite_flag, gen);
 }
 
@@ -392,14 +420,33 @@ __global__ void __launch_bounds__(kThreads) coarse_kernel(
 
 // Per-lane exact tests of one candidate primitive `p` (wave-uniform) on the
 // lane's kRowsPerLane pixels.  Triangles: MainState.cpp:257-298 restated on
-// the per-triangle constants (see TriRec); spheres: :300-327 on SphRec.
-__device__ __forceinline__ void test_primitive(int p, int n_tri, const TriRec* __restrict__ tri,
+// the per-triangle constants (see TriRec); `inside` (wave-uniform) means the
+// tile classifier proved every pixel of the tile passes the u/v tests, so
+// only the exact t is computed.  Spheres: :300-327 on SphRec.
+__device__ __forceinline__ void test_primitive(int p, bool inside, int n_tri,
+                                               const TriRec* __restrict__ tri,
                                                const SphRec* __restrict__ sph, double px,
                                                float pxf, const double* py, const float* pyf,
                                                float* closest, int* hit) {
     if (p < n_tri) {
         const TriRec r = tri[p];
         const double tx = px - r.v0x;
+        if (inside) {
+#pragma unroll
+            for (int j = 0; j < kRowsPerLane; ++j) {
+                const double ty = py[j] - r.v0y;
+                const double q2 = tx * r.e1y - ty * r.e1x;
+                const double q0 = ty * r.e1z - r.k0;
+                const double q1 = r.k1 - tx * r.e1z;
+                const double t = (r.e2x * q0 + r.e2y * q1 + r.e2z * q2) * r.inv_det;
+                const float tf = (float)t;
+                if (tf < closest[j]) {
+                    closest[j] = tf;
+                    hit[j] = p;
+                }
+            }
+            return;
+        }
 #pragma unroll
         for (int j = 0; j < kRowsPerLane; ++j) {
             const double ty = py[j] - r.v0y;
@@ -408,8 +455,8 @@ __device__ __forceinline__ void test_primitive(int p, int n_tri, const TriRec* _
             // v = ((d0*q0 + d1*q1) + d2*q2) * inv_det, d0 = d1 = +-0
             const double q2 = tx * r.e1y - ty * r.e1x;
             const double v = (r.dz * q2) * r.inv_det;
-            const bool inside = !(u < 0.0 || u > 1.0) && !(v < 0.0 || u + v > 1.0);
-            if (inside) {
+            const bool in = !(u < 0.0 || u > 1.0) && !(v < 0.0 || u + v > 1.0);
+            if (in) {
                 const double q0 = ty * r.e1z - r.k0;
                 const double q1 = r.k1 - tx * r.e1z;
                 const double t = (r.e2x * q0 + r.e2y * q1 + r.e2z * q2) * r.inv_det;
@@ -441,6 +488,31 @@ __device__ __forceinline__ void test_primitive(int p, int n_tri, const TriRec* _
     }
 }
 
+// Tile classification of one staged candidate against a 16x16 tile
+// [x0, x0+15] x [y0, y0+15] (fp32, conservative; see Cls).
+__device__ __forceinline__ void classify(const Cls& k, bool is_tri, float x0, float y0,
+                                         bool* keep, bool* inside) {
+    if (is_tri) {
+        const float xl = x0 - k.a.x, xh = (x0 + 15.0f) - k.a.x;
+        const float yl = y0 - k.a.y, yh = (y0 + 15.0f) - k.a.y;
+        const float u1 = k.a.z * xl, u2 = k.a.z * xh, u3 = k.a.w * yl, u4 = k.a.w * yh;
+        const float v1 = k.b.x * xl, v2 = k.b.x * xh, v3 = k.b.y * yl, v4 = k.b.y * yh;
+        const float umin = fminf(u1, u2) + fminf(u3, u4), umax = fmaxf(u1, u2) + fmaxf(u3, u4);
+        const float vmin = fminf(v1, v2) + fminf(v3, v4), vmax = fmaxf(v1, v2) + fmaxf(v3, v4);
+        const float g = k.b.z;
+        const bool out = umax < -g || umin > 1.0f + g || vmax < -g || vmin > 1.0f + g ||
+                         umin + vmin > 1.0f + g;
+        *keep = !out;
+        *inside = umin > g && umax < 1.0f - g && vmin > g && vmax < 1.0f - g &&
+                  umax + vmax < 1.0f - g;
+    } else {
+        const float dx = fmaxf(fmaxf(x0 - k.a.x, k.a.x - (x0 + 15.0f)), 0.0f);
+        const float dy = fmaxf(fmaxf(y0 - k.a.y, k.a.y - (y0 + 15.0f)), 0.0f);
+        *keep = !(dx * dx + dy * dy > k.a.z);
+        *inside = false;
+    }
+}
+
 __device__ __forceinline__ void store_pixel(void* __restrict__ out, int out_format, int64_t idx,
                                             int4v pix) {
     if (out_format == RT_FORMAT_I32X4)
@@ -460,12 +532,13 @@ __device__ __forceinline__ void store_pixel(void* __restrict__ out, int out_form
 template <int kMode>
 __global__ void __launch_bounds__(kThreads) trace_kernel(
     SceneDev scene, const TriRec* __restrict__ tri, const SphRec* __restrict__ sph,
-    const int4* __restrict__ boxes, const int* __restrict__ counts,
+    const int4* __restrict__ boxes, const Cls* __restrict__ cls, const int* __restrict__ counts,
     const int* __restrict__ lists, int cap, const unsigned* __restrict__ nonfinite_flag,
     unsigned gen, float4 dir, int width, int row_begin, int row_end, int n_bins_x, int n_cx,
     int out_format, void* __restrict__ out) {
     __shared__ int s_id[kStage];
     __shared__ int4 s_box[kStage];
+    __shared__ Cls s_cls[kStage];
     const int bin = blockIdx.x;
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
@@ -516,18 +589,21 @@ __global__ void __launch_bounds__(kThreads) trace_kernel(
             const int id = list[s0 + i];
             s_id[i] = id;
             s_box[i] = boxes[id];
+            s_cls[i] = cls[id];
         }
         __syncthreads();
         for (int c = 0; c < n; c += 64) {
             const int e = c + lane;
-            bool ov = false;
+            bool keep = false, inside = false;
             int id = 0;
             if (e < n) {
                 const int4 b = s_box[e];
                 id = s_id[e];
-                ov = b.x <= tx1 && b.z >= tile_x && b.y <= ty1 && b.w >= tile_y;
+                if (b.x <= tx1 && b.z >= tile_x && b.y <= ty1 && b.w >= tile_y)
+                    classify(s_cls[e], id < n_tri, (float)tile_x, (float)tile_y, &keep, &inside);
             }
-            unsigned long long m = __ballot(ov);
+            unsigned long long m = __ballot(keep);
+            const unsigned long long mi = __ballot(keep && inside);
             while (m) {
                 const int bit = __builtin_ctzll(m);
                 m &= m - 1;
@@ -536,7 +612,8 @@ __global__ void __launch_bounds__(kThreads) trace_kernel(
                     hit[0] = hit[0] > p ? hit[0] : -1;  // keep the walk alive
                     continue;
                 }
-                test_primitive(p, n_tri, tri, sph, px, pxf, py, pyf, closest, hit);
+                test_primitive(p, (mi >> bit) & 1ull, n_tri, tri, sph, px, pxf, py, pyf, closest,
+                               hit);
             }
         }
     }
@@ -691,7 +768,8 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
     const size_t tri_off = 0;
     const size_t sph_off = align_up(sizeof(TriRec) * (size_t)n_tri, 256);
     const size_t box_off = sph_off + align_up(sizeof(SphRec) * (size_t)s->num_spheres, 256);
-    const size_t cnt_off = box_off + align_up(sizeof(int4) * (size_t)n_prims, 256);
+    const size_t cls_off = box_off + align_up(sizeof(int4) * (size_t)n_prims, 256);
+    const size_t cnt_off = cls_off + align_up(sizeof(Cls) * (size_t)n_prims, 256);
     const size_t rec_need = cnt_off + align_up(sizeof(int) * (size_t)n_coarse, 256);
     int rc = ensure(&ctx->rec_buf, &ctx->rec_cap, rec_need);
     if (rc) return rc;
@@ -702,6 +780,7 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
     TriRec* tri = reinterpret_cast<TriRec*>(base + tri_off);
     SphRec* sph = reinterpret_cast<SphRec*>(base + sph_off);
     int4* boxes = reinterpret_cast<int4*>(base + box_off);
+    Cls* clsv = reinterpret_cast<Cls*>(base + cls_off);
     int* counts = reinterpret_cast<int*>(base + cnt_off);
     int* lists = static_cast<int*>(ctx->list_buf);
     // generation-stamped non-finite flag: no per-launch memset needed
@@ -712,7 +791,7 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
 
     if (n_prims > 0) {
         prep_kernel<<<dim3((n_prims + kThreads - 1) / kThreads), dim3(kThreads), 0, stream>>>(
-            sd, dir, width, row_begin, row_end, tri, sph, boxes, ctx->flag, ctx->gen);
+            sd, dir, width, row_begin, row_end, tri, sph, boxes, clsv, ctx->flag, ctx->gen);
         HIP_TRY(hipGetLastError());
     }
     if (pe) HIP_TRY(hipEventRecord(pe[1], stream));
@@ -723,7 +802,7 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
     auto kern = ctx->trace_mode == 1 ? trace_kernel<1>
               : ctx->trace_mode == 2 ? trace_kernel<2> : trace_kernel<0>;
     kern<<<dim3((unsigned)n_bins), dim3(kThreads), 0, stream>>>(
-        sd, tri, sph, boxes, counts, lists, cap, ctx->flag, ctx->gen, dir, width, row_begin,
+        sd, tri, sph, boxes, clsv, counts, lists, cap, ctx->flag, ctx->gen, dir, width, row_begin,
         row_end, n_bins_x, n_cx, fmt, out);
     HIP_TRY(hipGetLastError());
     if (pe) HIP_TRY(hipEventRecord(pe[3], stream));
@@ -944,13 +1023,15 @@ int rt_selftest_fp32(rt_ctx* ctx, const float* host_in, int32_t n, float* host_s
 // int32[4] (x0, y0, x1, y1) and returns 1 when the triangle is valid.
 int rt_debug_triangle_box(const float v0[3], const float v1[3], const float v2[3],
                           const float dir[4], int32_t width, int32_t row_begin, int32_t row_end,
-                          int32_t box_out[4]) {
+                          int32_t box_out[4], float cls_out[8]) {
     TriRec r{};
     Box b{};
+    Cls k{};
     bool bad = false;
     const bool ok = prep_triangle(v0, v1, v2, dir[0], dir[1], dir[2], width, row_begin, row_end,
-                                  &r, &b, &bad);
+                                  &r, &b, &k, &bad);
     box_out[0] = b.x0; box_out[1] = b.y0; box_out[2] = b.x1; box_out[3] = b.y1;
+    if (cls_out) std::memcpy(cls_out, &k, sizeof k);
     return ok ? 1 : 0;
 }
 
@@ -962,13 +1043,16 @@ int rt_debug_set_trace_mode(rt_ctx* ctx, int mode) {
 }
 
 int rt_debug_sphere_box(const float origin[4], float radius, const float dir[4], int32_t width,
-                        int32_t row_begin, int32_t row_end, int32_t box_out[4]) {
+                        int32_t row_begin, int32_t row_end, int32_t box_out[4],
+                        float cls_out[8]) {
     SphRec r{};
     Box b{};
+    Cls k{};
     bool bad = false;
     prep_sphere(origin, radius, dir[0], dir[1], dir[2], dir[3], width, row_begin, row_end, &r, &b,
-                &bad);
+                &k, &bad);
     box_out[0] = b.x0; box_out[1] = b.y0; box_out[2] = b.x1; box_out[3] = b.y1;
+    if (cls_out) std::memcpy(cls_out, &k, sizeof k);
     return bad ? 0 : 1;
 }
 

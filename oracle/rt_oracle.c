@@ -613,6 +613,38 @@ void orc_trace_rows_mt(int32_t width, int32_t height, const int32_t* rows, int32
     for (int i = 0; i < n_threads; ++i) pthread_join(th[i], NULL);
 }
 
+/* Hit masks of one triangle / one sphere over a pixel rectangle (implicit
+ * origins (x, y, 0, 1)), for the culling-bound tests. */
+void orc_tri_grid(const float v0[3], const float v1[3], const float v2[3], const float dir[4],
+                  int32_t x0, int32_t y0, int32_t w, int32_t h, uint8_t* hits) {
+    const double a[3] = {v0[0], v0[1], v0[2]}, b[3] = {v1[0], v1[1], v1[2]},
+                 c[3] = {v2[0], v2[1], v2[2]}, d[3] = {dir[0], dir[1], dir[2]};
+    for (int32_t j = 0; j < h; ++j)
+        for (int32_t i = 0; i < w; ++i) {
+            const double o[3] = {(double)(float)(x0 + i), (double)(float)(y0 + j), 0.0};
+            double t, u, v;
+            hits[(int64_t)j * w + i] = (uint8_t)orc_intersect_tri(o, d, a, b, c, &t, &u, &v);
+        }
+}
+
+void orc_sphere_grid(const float centre[4], float radius, const float dir[4], int32_t x0,
+                     int32_t y0, int32_t w, int32_t h, uint8_t* hits) {
+    for (int32_t j = 0; j < h; ++j)
+        for (int32_t i = 0; i < w; ++i) {
+            const float o[4] = {(float)(x0 + i), (float)(y0 + j), 0.0f, 1.0f};
+            /* "hit" = the reference would consider it (t0 != 0 is a later test) */
+            const float L[4] = {centre[0] - o[0], centre[1] - o[1], centre[2] - o[2],
+                                centre[3] - o[3]};
+            const float tca = dot4(L, dir);
+            uint8_t hit = 0;
+            if (!(tca < 0)) {
+                const float d2 = dot4(L, L) - tca * tca;
+                hit = !(d2 > radius * radius);
+            }
+            hits[(int64_t)j * w + i] = hit;
+        }
+}
+
 uint64_t orc_fnv1a_i32(const int32_t* v, int64_t n) {
     uint64_t h = 0xcbf29ce484222325ull;
     for (int64_t i = 0; i < n; ++i) {

@@ -104,6 +104,14 @@ void orc_trace_cl32(int32_t width, int32_t height, const float ray_dir[4],
                     int32_t n_cubes, const float* cube_vertices,
                     const float* cube_colours, int32_t* out);
 
+/* Per-pixel hit masks of one triangle (orc_intersect_tri == 1) / one sphere
+ * (passes the tca and distance tests) over [x0,x0+w) x [y0,y0+h). */
+void orc_tri_grid(const float v0[3], const float v1[3], const float v2[3],
+                  const float dir[4], int32_t x0, int32_t y0, int32_t w, int32_t h,
+                  uint8_t* hits);
+void orc_sphere_grid(const float centre[4], float radius, const float dir[4],
+                     int32_t x0, int32_t y0, int32_t w, int32_t h, uint8_t* hits);
+
 /* FNV-1a-64 over the int32 stream (SURVEY.md §8c known-answer format). */
 uint64_t orc_fnv1a_i32(const int32_t* v, int64_t n);
 

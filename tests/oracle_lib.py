@@ -51,6 +51,8 @@ def _load() -> ctypes.CDLL:
         "orc_trace_rows_mt": (None, [_i32, _i32, _vp, _i32, _vp, _vp, _i32, _vp, _vp, _vp, _i32,
                                      _vp, _vp, _vp, _i32]),
         "orc_trace_cl32": (None, [_i32, _i32, _vp, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _vp]),
+        "orc_tri_grid": (None, [_vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp]),
+        "orc_sphere_grid": (None, [_vp, _f32, _vp, _i32, _i32, _i32, _i32, _vp]),
         "orc_fnv1a_i32": (ctypes.c_uint64, [_vp, ctypes.c_int64]),
         "orc_pack_rgba8": (None, [_vp, ctypes.c_int64, _vp]),
     }
@@ -166,6 +168,20 @@ class Oracle:
         d = np.ascontiguousarray(direction, np.float32)
         c = np.ascontiguousarray(centre, np.float32)
         return float(self.lib.orc_intersect_sphere(_p(o), _p(d), radius, _p(c)))
+
+    def tri_grid(self, v0, v1, v2, direction, x0, y0, w, h) -> np.ndarray:
+        a = [np.ascontiguousarray(v, np.float32)[:3].copy() for v in (v0, v1, v2)]
+        d = np.ascontiguousarray(direction, np.float32)
+        out = np.zeros((h, w), np.uint8)
+        self.lib.orc_tri_grid(_p(a[0]), _p(a[1]), _p(a[2]), _p(d), x0, y0, w, h, _p(out))
+        return out
+
+    def sphere_grid(self, centre, radius, direction, x0, y0, w, h) -> np.ndarray:
+        c = np.ascontiguousarray(centre, np.float32)
+        d = np.ascontiguousarray(direction, np.float32)
+        out = np.zeros((h, w), np.uint8)
+        self.lib.orc_sphere_grid(_p(c), float(radius), _p(d), x0, y0, w, h, _p(out))
+        return out
 
     def cube(self, ops) -> np.ndarray:
         v = np.zeros((36, 4), np.float32)

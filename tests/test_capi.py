@@ -1,0 +1,73 @@
+"""The C-ABI boundary (include/rt_hip.h): library loads, exports every
+declared symbol, and validates arguments without a GPU."""
+import ctypes
+import re
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+REPO = Path(__file__).resolve().parents[1]
+HEADER = REPO / "include" / "rt_hip.h"
+
+
+def declared_functions():
+    text = HEADER.read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(rt_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_declares_the_boundary():
+    names = declared_functions()
+    for required in ("rt_init", "rt_render", "rt_render_device", "rt_destroy",
+                     "rt_error_string"):
+        assert required in names
+
+
+def test_library_exports_every_declared_symbol(pkg):
+    lib = ctypes.CDLL(str(pkg.library_path()))
+    missing = [n for n in declared_functions() if not hasattr(lib, n)]
+    assert not missing, missing
+    assert set(declared_functions()) == set(pkg.EXPORTED_SYMBOLS)
+
+
+def test_abi_version(pkg):
+    assert pkg.library().rt_abi_version() == 1
+
+
+def test_error_strings(pkg):
+    lib = pkg.library()
+    for code in (0, -1, -2, -3, -4, -5):
+        assert lib.rt_error_string(code)
+    assert lib.rt_error_string(-99) == b"unknown error"
+
+
+def test_argument_validation_without_gpu(pkg):
+    lib = pkg.library()
+    scene = pkg.Scene()
+    c = scene.as_c()
+    out = np.zeros(16, np.int32)
+    d = pkg.primary_ray_dir()
+    # NULL context is rejected before any HIP call
+    assert lib.rt_render(None, ctypes.byref(c), d.ctypes.data, None, 2, 2, 0, 2, 0,
+                         out.ctypes.data, None) == pkg.RT_ERR_INVALID_ARG
+    assert lib.rt_render_device(None, ctypes.byref(c), d.ctypes.data, None, 2, 2, 0, 2, 0, 0,
+                                out.ctypes.data, None) == pkg.RT_ERR_INVALID_ARG
+    assert lib.rt_init(0, None) == pkg.RT_ERR_INVALID_ARG
+
+
+def test_init_without_gpu_reports_no_device(pkg):
+    torch = pytest.importorskip("torch")
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    with pytest.raises(pkg.RtError) as e:
+        pkg.RayTracer(0)
+    assert e.value.status == pkg.RT_ERR_NO_DEVICE
+
+
+def test_scene_helpers_validate(pkg):
+    lib = pkg.library()
+    n = ctypes.c_int32()
+    assert lib.rt_scene_reference(4, 1, None, None, None, None, None, ctypes.byref(n),
+                                  ctypes.byref(n)) == -1
+    assert lib.rt_scene_synthetic(0, 10, 1, 1, 1, 1.0, None, None, None, None, None) == -1

@@ -1,0 +1,84 @@
+"""Multi-rank row-band path on the CPU: world_size 2 over gloo.  Each rank
+renders its band (the oracle stands in for the per-GPU band renderer -- test
+infrastructure only), the scene is broadcast from rank 0 and the frame is
+gathered on rank 0 with the same rowbands.py code the GPU path uses."""
+import os
+import socket
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+REPO = Path(__file__).resolve().parents[1]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, width, height, scene_id, result_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, str(REPO))
+    sys.path.insert(0, str(REPO / "tests"))
+    import torch
+    import torch.distributed as dist
+
+    import __graft_entry__
+    from oracle_lib import Oracle
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        pkg = __graft_entry__.load_package()
+        from opencl_ray_tracer_amd import rowbands
+
+        oracle = Oracle()
+        arrays = None
+        if rank == 0:
+            sc = oracle.scene_reference(scene_id, 1)
+            arrays = {k: getattr(sc, k) for k in rowbands.SCENE_FIELDS}
+        scene = rowbands.broadcast_scene(arrays, 0, torch.device("cpu"))
+        ns = pkg.Scene(*(scene[k].numpy() for k in rowbands.SCENE_FIELDS))
+
+        def render_band(rb, re):
+            return torch.from_numpy(oracle.trace(ns, width, height, rows=(rb, re)))
+
+        frame = rowbands.render_distributed(render_band, height, world, rank)
+        if rank == 0:
+            np.save(result_path, frame.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("height,scene_id", [(480, 1), (97, 3)])
+def test_two_rank_row_bands_gloo(tmp_path, oracle, height, scene_id):
+    import torch.multiprocessing as mp
+
+    width, world = 640, 2
+    out = tmp_path / "frame.npy"
+    mp.spawn(_worker, args=(world, _free_port(), width, height, scene_id, str(out)),
+             nprocs=world, join=True)
+    frame = np.load(out)
+    want = oracle.trace(oracle.scene_reference(scene_id, 1), width, height)
+    assert np.array_equal(frame, want)
+
+
+def test_band_rows_partition():
+    sys.path.insert(0, str(REPO))
+    import __graft_entry__
+    __graft_entry__.load_package()
+    from opencl_ray_tracer_amd.rowbands import band_rows
+
+    for h in (1, 7, 480, 4096, 4097):
+        for world in (1, 2, 3, 4, 8):
+            if world > h:
+                continue
+            bands = [band_rows(h, world, r) for r in range(world)]
+            assert bands[0][0] == 0 and bands[-1][1] == h
+            assert all(a[1] == b[0] for a, b in zip(bands, bands[1:]))
+            sizes = [e - b for b, e in bands]
+            assert max(sizes) - min(sizes) <= 1

@@ -1,0 +1,159 @@
+"""Host-side product code of librt_hip.so, on the CPU (no GPU needed):
+scene packing vs the oracle, and the culling bounds of the prep kernel
+(same __host__ __device__ code) proven conservative against the oracle's
+per-pixel tests (MainState.cpp:257-327)."""
+import numpy as np
+import pytest
+
+RAY_DIR = np.array([0.0, 0.0, -1.0, -1.0], np.float32)
+
+
+def _bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.uint32)
+
+
+@pytest.mark.parametrize("scene_id", [1, 2, 3])
+def test_reference_scenes_match_oracle(pkg, oracle, scene_id):
+    got = pkg.Scene.reference(scene_id, 1)
+    want = oracle.scene_reference(scene_id, 1)
+    for k in ("sphere_origins", "sphere_radius", "sphere_colours", "cube_vertices",
+              "cube_colours"):
+        assert np.array_equal(_bits(getattr(got, k)), _bits(getattr(want, k))), k
+
+
+@pytest.mark.parametrize("args", [(512, 512, 4, 1, 1, 0.8), (1920, 1080, 16, 4, 2, 3.0),
+                                  (4096, 4096, 256, 64, 3, 6.4), (97, 31, 0, 5, 9, 1.0)])
+def test_synthetic_scene_matches_oracle(pkg, oracle, args):
+    w, h, n, m, seed, k = args
+    got = pkg.Scene.synthetic(w, h, n, m, seed=seed, k=k)
+    want = oracle.scene_synthetic(w, h, n, m, seed, k)
+    for key in ("sphere_origins", "sphere_radius", "sphere_colours", "cube_vertices",
+                "cube_colours"):
+        assert np.array_equal(_bits(getattr(got, key)), _bits(getattr(want, key))), key
+
+
+def test_cube_ops_match_oracle(pkg, oracle):
+    rng = np.random.default_rng(3)
+    for _ in range(200):
+        ops = []
+        for _ in range(int(rng.integers(1, 6))):
+            kind = ["scale", "rotate", "translate"][int(rng.integers(0, 3))]
+            lo, hi = {"scale": (0.01, 80), "rotate": (-7, 7), "translate": (-700, 700)}[kind]
+            ops.append((kind, *rng.uniform(lo, hi, 3)))
+        assert np.array_equal(_bits(pkg.cube_packed(ops)), _bits(oracle.cube(ops)))
+
+
+def test_primary_ray_dir_and_angles(pkg, oracle):
+    assert np.array_equal(pkg.primary_ray_dir(), RAY_DIR)
+    for d in (0.0, 30.0, 80.0, 160.0, 210.0, 250.0, 359.0):
+        assert np.float32(pkg.deg_to_rad(d)) == np.float32(oracle.deg2rad(d))
+
+
+def test_pack_rgba8_matches_oracle(pkg, oracle):
+    rng = np.random.default_rng(1)
+    frame = rng.integers(-300, 600, (37, 53, 4)).astype(np.int32)
+    assert np.array_equal(pkg.pack_rgba8(frame), oracle.pack_rgba8(frame))
+    # (uint8) wrap of r, g, b; alpha forced opaque (MainState.cpp:1026-1036)
+    px = pkg.pack_rgba8(np.array([[[257, -1, 255, 7]]], np.int32))[0, 0]
+    assert px == (1 | (255 << 8) | (255 << 16) | (255 << 24))
+
+
+# ---------------------------------------------------------------------------
+# culling bounds
+# ---------------------------------------------------------------------------
+def classify_tile(cls, is_tri, x0, y0):
+    """numpy float32 mirror of the trace kernel's classify() (rt_device.hip)."""
+    f = np.float32
+    a = cls[:4].astype(np.float32)
+    b = cls[4:].astype(np.float32)
+    x0, y0 = f(x0), f(y0)
+    if is_tri:
+        xl, xh = x0 - a[0], (x0 + f(15)) - a[0]
+        yl, yh = y0 - a[1], (y0 + f(15)) - a[1]
+        u1, u2, u3, u4 = a[2] * xl, a[2] * xh, a[3] * yl, a[3] * yh
+        v1, v2, v3, v4 = b[0] * xl, b[0] * xh, b[1] * yl, b[1] * yh
+        umin, umax = min(u1, u2) + min(u3, u4), max(u1, u2) + max(u3, u4)
+        vmin, vmax = min(v1, v2) + min(v3, v4), max(v1, v2) + max(v3, v4)
+        g = b[2]
+        out = (umax < -g or umin > f(1) + g or vmax < -g or vmin > f(1) + g
+               or umin + vmin > f(1) + g)
+        inside = (umin > g and umax < f(1) - g and vmin > g and vmax < f(1) - g
+                  and umax + vmax < f(1) - g)
+        return not out, bool(inside)
+    dx = max(max(x0 - a[0], a[0] - (x0 + f(15))), f(0))
+    dy = max(max(y0 - a[1], a[1] - (y0 + f(15))), f(0))
+    return not (dx * dx + dy * dy > a[2]), False
+
+
+def random_triangles(rng, w, h, n):
+    tris = []
+    for i in range(n):
+        kind = i % 5
+        c = rng.uniform([-20, -20, -120], [w + 20, h + 20, 20])
+        if kind == 0:    # ordinary
+            v = c + rng.uniform(-60, 60, (3, 3))
+        elif kind == 1:  # sliver: nearly collinear in xy
+            d = rng.uniform(-80, 80, 3)
+            v = np.stack([c, c + d, c + d * rng.uniform(0.2, 0.8) + rng.uniform(-1e-3, 1e-3, 3)])
+        elif kind == 2:  # tiny
+            v = c + rng.uniform(-0.05, 0.05, (3, 3))
+        elif kind == 3:  # huge, mostly off-frame
+            v = c + rng.uniform(-3000, 3000, (3, 3))
+        else:            # axis-aligned edges through pixel centres
+            x, y = np.floor(c[:2])
+            s = float(rng.integers(1, 40))
+            v = np.array([[x, y, c[2]], [x + s, y, c[2] - 3], [x, y + s, c[2] + 2]])
+        tris.append(v.astype(np.float32))
+    return tris
+
+
+@pytest.mark.parametrize("band", [(0, 160), (37, 121)])
+def test_triangle_box_and_tile_classifier_are_conservative(pkg, oracle, band):
+    w, h = 176, 160
+    rb, re = band
+    rng = np.random.default_rng(7 + rb)
+    n_inside_tiles = n_skip_tiles = 0
+    for v in random_triangles(rng, w, h, 150):
+        ok, box, cls = pkg.debug_triangle_prep(v[0], v[1], v[2], RAY_DIR, w, rb, re)
+        hits = oracle.tri_grid(v[0], v[1], v[2], RAY_DIR, 0, rb, w, re - rb)
+        if not ok:
+            assert not hits.any()
+            continue
+        ys, xs = np.nonzero(hits)
+        if len(xs):
+            assert box[0] <= xs.min() and xs.max() <= box[2]
+            assert box[1] <= ys.min() + rb and ys.max() + rb <= box[3]
+        for ty in range(rb, re, 16):
+            for tx in range(0, w, 16):
+                keep, inside = classify_tile(cls, True, tx, ty)
+                tile = hits[ty - rb:ty - rb + 16, tx:tx + 16]
+                if not keep:
+                    n_skip_tiles += 1
+                    assert not tile.any(), (v, tx, ty)
+                if inside:
+                    n_inside_tiles += 1
+                    assert tile.all(), (v, tx, ty)
+    assert n_inside_tiles > 0 and n_skip_tiles > 0  # the classifier does something
+
+
+def test_sphere_box_and_tile_classifier_are_conservative(pkg, oracle):
+    w, h = 160, 128
+    rng = np.random.default_rng(11)
+    for i in range(120):
+        c = np.float32([rng.uniform(-30, w + 30), rng.uniform(-30, h + 30),
+                        rng.uniform(-150, 10), [1.0, 0.5, 3.0][i % 3]])
+        r = np.float32([0.0, 1e-3, 0.7, 5.0, 25.0, 90.0][i % 6] * rng.uniform(0.5, 1.5))
+        ok, box, cls = pkg.debug_sphere_prep(c, r, RAY_DIR, w, 0, h)
+        assert ok
+        hits = oracle.sphere_grid(c, r, RAY_DIR, 0, 0, w, h)
+        ys, xs = np.nonzero(hits)
+        if len(xs):
+            assert box[0] <= xs.min() and xs.max() <= box[2]
+            assert box[1] <= ys.min() and ys.max() <= box[3]
+        elif box[0] > box[2]:
+            continue
+        for ty in range(0, h, 16):
+            for tx in range(0, w, 16):
+                keep, _ = classify_tile(cls, False, tx, ty)
+                if not keep:
+                    assert not hits[ty:ty + 16, tx:tx + 16].any(), (c, r, tx, ty)
