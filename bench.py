@@ -49,7 +49,7 @@ def parse():
     ap.add_argument("--seed", type=int, default=3)
     ap.add_argument("--k", type=float, default=None, help="object scale (default width/640)")
     ap.add_argument("--format", choices=sorted(BYTES_PER_RAY), default="i32x4")
-    ap.add_argument("--cpu-rows", type=int, default=16,
+    ap.add_argument("--cpu-rows", type=int, default=4,
                     help="CPU baseline samples every Nth row of rank 0's band")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -167,12 +167,23 @@ __host__ __device__ inline bool prep_triangle(const float* a, const float* b, co
                           ty_max * (fabs(p1) + fabs(e1[0] * dz))) * fabs(inv_det);
         const double err = (32.0 * eps + 4.0 * rho) * s + 32.0 * eps;
         const double g = 2.0 * err + 8.0 * eps * s + 32.0 * eps;
-        // fp32 tile-classifier planes and their margin (fp32 rounding of the
-        // coefficients and of the corner evaluation, 2^-24 each, x32 slack)
+        // fp32 classifier planes and their margin.  The classifier only ever
+        // sees pixels of 16x16 tiles that overlap the box, so |x - v0x| and
+        // |y - v0y| are bounded by the padded box plus one tile: the margin
+        // covers the fp64 test's rounding there (err_loc) and the fp32
+        // rounding of the coefficients and of the plane evaluation (2^-24
+        // each, x32 slack).
+        const double padx0 = 8.0 * (mxx - mnx) * g + 0.5, pady0 = 8.0 * (mxy - mny) * g + 0.5;
+        const double tx_loc = fmax(fabs(mnx - padx0 - 32.0 - v0[0]), fabs(mxx + padx0 + 32.0 - v0[0])) + 1.0;
+        const double ty_loc = fmax(fabs(mny - pady0 - 32.0 - v0[1]), fabs(mxy + pady0 + 32.0 - v0[1])) + 1.0;
+        const double s_loc = (tx_loc * (fabs(p0) + fabs(e1[1] * dz)) +
+                              ty_loc * (fabs(p1) + fabs(e1[0] * dz))) * fabs(inv_det);
+        const double err_loc = (32.0 * eps + 4.0 * rho) * s_loc + 32.0 * eps;
+        const double g_loc = 2.0 * err_loc + 8.0 * eps * s_loc + 32.0 * eps;
         const double au = p0 * inv_det, bu = p1 * inv_det;
         const double av = dz * e1[1] * inv_det, bv = -(dz * e1[0]) * inv_det;
-        const double suv = (fabs(au) + fabs(av)) * tx_max + (fabs(bu) + fabs(bv)) * ty_max;
-        const double gm = g + 32.0 * 5.9604644775390625e-08 * suv + 1e-6;
+        const double suv = (fabs(au) + fabs(av)) * tx_loc + (fabs(bu) + fabs(bv)) * ty_loc;
+        const double gm = g_loc + 32.0 * 5.9604644775390625e-08 * suv + 1e-6;
         cls->a = make_float4((float)v0[0], (float)v0[1], (float)au, (float)bu);
         cls->b = make_float4((float)av, (float)bv, (float)(gm * (1.0 + 1e-6)), 0.0f);
         const double padx = 8.0 * (mxx - mnx) * g + 0.5;
@@ -423,7 +434,7 @@ __global__ void __launch_bounds__(kThreads) coarse_kernel(
 // the per-triangle constants (see TriRec); `inside` (wave-uniform) means the
 // tile classifier proved every pixel of the tile passes the u/v tests, so
 // only the exact t is computed.  Spheres: :300-327 on SphRec.
-__device__ __forceinline__ void test_primitive(int p, bool inside, int n_tri,
+__device__ __forceinline__ void test_primitive(int p, bool inside, const Cls& k, int n_tri,
                                                const TriRec* __restrict__ tri,
                                                const SphRec* __restrict__ sph, double px,
                                                float pxf, const double* py, const float* pyf,
@@ -447,16 +458,33 @@ __device__ __forceinline__ void test_primitive(int p, bool inside, int n_tri,
             }
             return;
         }
+        // Partial tile: classify each pixel on the fp32 planes first (same
+        // margin as the tile classifier); only pixels inside the margin band
+        // of an edge run the full fp64 u/v test, proven-inside pixels compute
+        // t only, proven-outside pixels are done.
+        const float xl = pxf - k.a.x;
+        const float ux = k.a.z * xl, vx = k.b.x * xl;
+        const float g = k.b.z;
 #pragma unroll
         for (int j = 0; j < kRowsPerLane; ++j) {
+            const float yl = pyf[j] - k.a.y;
+            const float ul = ux + k.a.w * yl;
+            const float vl = vx + k.b.y * yl;
+            const float wl = ul + vl;
+            const bool out = ul < -g || ul > 1.0f + g || vl < -g || vl > 1.0f + g || wl > 1.0f + g;
+            const bool in = ul > g && ul < 1.0f - g && vl > g && vl < 1.0f - g && wl < 1.0f - g;
+            if (out) continue;
             const double ty = py[j] - r.v0y;
-            // u = ((tx*p0 + ty*p1) + tz*p2) * inv_det, tz*p2 == +-0 for d = (0,0,D)
-            const double u = (tx * r.p0 + ty * r.p1) * r.inv_det;
-            // v = ((d0*q0 + d1*q1) + d2*q2) * inv_det, d0 = d1 = +-0
             const double q2 = tx * r.e1y - ty * r.e1x;
-            const double v = (r.dz * q2) * r.inv_det;
-            const bool in = !(u < 0.0 || u > 1.0) && !(v < 0.0 || u + v > 1.0);
-            if (in) {
+            bool pass = in;
+            if (!in) {
+                // u = ((tx*p0 + ty*p1) + tz*p2) * inv_det, tz*p2 == +-0 for d = (0,0,D)
+                const double u = (tx * r.p0 + ty * r.p1) * r.inv_det;
+                // v = ((d0*q0 + d1*q1) + d2*q2) * inv_det, d0 = d1 = +-0
+                const double v = (r.dz * q2) * r.inv_det;
+                pass = !(u < 0.0 || u > 1.0) && !(v < 0.0 || u + v > 1.0);
+            }
+            if (pass) {
                 const double q0 = ty * r.e1z - r.k0;
                 const double q1 = r.k1 - tx * r.e1z;
                 const double t = (r.e2x * q0 + r.e2y * q1 + r.e2z * q2) * r.inv_det;
@@ -486,6 +514,10 @@ __device__ __forceinline__ void test_primitive(int p, bool inside, int n_tri,
             }
         }
     }
+}
+
+__device__ __forceinline__ float readlane_f(float v, int lane) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), lane));
 }
 
 // Tile classification of one staged candidate against a 16x16 tile
@@ -596,11 +628,14 @@ __global__ void __launch_bounds__(kThreads) trace_kernel(
             const int e = c + lane;
             bool keep = false, inside = false;
             int id = 0;
+            Cls kc{};
             if (e < n) {
                 const int4 b = s_box[e];
                 id = s_id[e];
-                if (b.x <= tx1 && b.z >= tile_x && b.y <= ty1 && b.w >= tile_y)
-                    classify(s_cls[e], id < n_tri, (float)tile_x, (float)tile_y, &keep, &inside);
+                if (b.x <= tx1 && b.z >= tile_x && b.y <= ty1 && b.w >= tile_y) {
+                    kc = s_cls[e];
+                    classify(kc, id < n_tri, (float)tile_x, (float)tile_y, &keep, &inside);
+                }
             }
             unsigned long long m = __ballot(keep);
             const unsigned long long mi = __ballot(keep && inside);
@@ -612,8 +647,13 @@ __global__ void __launch_bounds__(kThreads) trace_kernel(
                     hit[0] = hit[0] > p ? hit[0] : -1;  // keep the walk alive
                     continue;
                 }
-                test_primitive(p, (mi >> bit) & 1ull, n_tri, tri, sph, px, pxf, py, pyf, closest,
-                               hit);
+                Cls k;
+                k.a = make_float4(readlane_f(kc.a.x, bit), readlane_f(kc.a.y, bit),
+                                  readlane_f(kc.a.z, bit), readlane_f(kc.a.w, bit));
+                k.b = make_float4(readlane_f(kc.b.x, bit), readlane_f(kc.b.y, bit),
+                                  readlane_f(kc.b.z, bit), 0.0f);
+                test_primitive(p, (mi >> bit) & 1ull, k, n_tri, tri, sph, px, pxf, py, pyf,
+                               closest, hit);
             }
         }
     }

@@ -107,6 +107,24 @@ def random_triangles(rng, w, h, n):
     return tris
 
 
+def classify_pixels(cls, xs, ys):
+    """numpy float32 mirror of test_primitive's per-pixel pre-classification
+    (partial tiles): returns (out, inside) masks."""
+    f = np.float32
+    a = cls[:4].astype(np.float32)
+    b = cls[4:].astype(np.float32)
+    xl = xs.astype(np.float32) - a[0]
+    ux, vx = a[2] * xl, b[0] * xl
+    yl = ys.astype(np.float32) - a[1]
+    ul = ux + a[3] * yl
+    vl = vx + b[1] * yl
+    wl = ul + vl
+    g = b[2]
+    out = (ul < -g) | (ul > f(1) + g) | (vl < -g) | (vl > f(1) + g) | (wl > f(1) + g)
+    inside = (ul > g) & (ul < f(1) - g) & (vl > g) & (vl < f(1) - g) & (wl < f(1) - g)
+    return out, inside
+
+
 @pytest.mark.parametrize("band", [(0, 160), (37, 121)])
 def test_triangle_box_and_tile_classifier_are_conservative(pkg, oracle, band):
     w, h = 176, 160
@@ -123,8 +141,19 @@ def test_triangle_box_and_tile_classifier_are_conservative(pkg, oracle, band):
         if len(xs):
             assert box[0] <= xs.min() and xs.max() <= box[2]
             assert box[1] <= ys.min() + rb and ys.max() + rb <= box[3]
+        # per-pixel pre-classification of every pixel inside the padded box
+        x0, x1 = max(box[0] - 16, 0), min(box[2] + 16, w - 1)
+        y0, y1 = max(box[1] - 16, rb), min(box[3] + 16, re - 1)
+        if x0 <= x1 and y0 <= y1:
+            ys, xs = np.mgrid[y0:y1 + 1, x0:x1 + 1]
+            out_px, in_px = classify_pixels(cls, xs, ys)
+            sub = hits[y0 - rb:y1 - rb + 1, x0:x1 + 1].astype(bool)
+            assert not (out_px & sub).any(), v
+            assert not (in_px & ~sub).any(), v
         for ty in range(rb, re, 16):
             for tx in range(0, w, 16):
+                if box[0] > tx + 15 or box[2] < tx or box[1] > ty + 15 or box[3] < ty:
+                    continue  # the kernel classifies only tiles the box touches
                 keep, inside = classify_tile(cls, True, tx, ty)
                 tile = hits[ty - rb:ty - rb + 16, tx:tx + 16]
                 if not keep:
