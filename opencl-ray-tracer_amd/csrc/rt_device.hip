@@ -38,12 +38,28 @@
 
 namespace {
 
-constexpr int kBinW = 32;         // bin = workgroup tile, pixels
-constexpr int kBinH = 32;
+// Build-time geometry / feature knobs (A/B variants: scripts/variants.sh).
+#ifndef RT_TILE_W
+#define RT_TILE_W 16              // wave tile width (lanes per row)
+#endif
+#ifndef RT_ROWS
+#define RT_ROWS 4                 // pixels per lane (rows, 64/RT_TILE_W apart)
+#endif
+#ifndef RT_TILECLS
+#define RT_TILECLS 1              // per-tile plane classification of candidates
+#endif
+#ifndef RT_PIXCLS
+#define RT_PIXCLS 0               // per-pixel fp32 pre-classification
+#endif
+constexpr int kWaveTile = RT_TILE_W;                       // wave tile width
+constexpr int kRowsPerLane = RT_ROWS;
+constexpr int kLaneRows = 64 / RT_TILE_W;                  // lane rows per pass
+constexpr int kWaveTileH = kLaneRows * RT_ROWS;            // wave tile height
+constexpr int kBinW = 2 * kWaveTile;  // bin = workgroup tile (2x2 wave tiles)
+constexpr int kBinH = 2 * kWaveTileH;
 constexpr int kCoarse = 64;       // coarse bin (candidate list) edge, pixels
 constexpr int kStage = 256;       // candidate entries staged in LDS per pass
-constexpr int kWaveTile = 16;     // each wave owns a 16x16 quadrant of the bin
-constexpr int kRowsPerLane = 4;   // lane rows y0, y0+4, y0+8, y0+12
+static_assert(64 % kBinW == 0 && 64 % kBinH == 0, "bins must tile a coarse bin");
 constexpr int kThreads = 256;
 constexpr double kEpsilon = 0.000001;      // MainState.cpp:15
 constexpr float kFar = 300000.0f;          // MainState.cpp:345
@@ -462,11 +478,14 @@ __device__ __forceinline__ void test_primitive(int p, bool inside, const Cls& k,
         // margin as the tile classifier); only pixels inside the margin band
         // of an edge run the full fp64 u/v test, proven-inside pixels compute
         // t only, proven-outside pixels are done.
+#if RT_PIXCLS
         const float xl = pxf - k.a.x;
         const float ux = k.a.z * xl, vx = k.b.x * xl;
         const float g = k.b.z;
+#endif
 #pragma unroll
         for (int j = 0; j < kRowsPerLane; ++j) {
+#if RT_PIXCLS
             const float yl = pyf[j] - k.a.y;
             const float ul = ux + k.a.w * yl;
             const float vl = vx + k.b.y * yl;
@@ -474,6 +493,9 @@ __device__ __forceinline__ void test_primitive(int p, bool inside, const Cls& k,
             const bool out = ul < -g || ul > 1.0f + g || vl < -g || vl > 1.0f + g || wl > 1.0f + g;
             const bool in = ul > g && ul < 1.0f - g && vl > g && vl < 1.0f - g && wl < 1.0f - g;
             if (out) continue;
+#else
+            const bool in = false;
+#endif
             const double ty = py[j] - r.v0y;
             const double q2 = tx * r.e1y - ty * r.e1x;
             bool pass = in;
@@ -516,7 +538,7 @@ __device__ __forceinline__ void test_primitive(int p, bool inside, const Cls& k,
     }
 }
 
-__device__ __forceinline__ float readlane_f(float v, int lane) {
+[[maybe_unused]] __device__ __forceinline__ float readlane_f(float v, int lane) {
     return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), lane));
 }
 
@@ -524,9 +546,10 @@ __device__ __forceinline__ float readlane_f(float v, int lane) {
 // [x0, x0+15] x [y0, y0+15] (fp32, conservative; see Cls).
 __device__ __forceinline__ void classify(const Cls& k, bool is_tri, float x0, float y0,
                                          bool* keep, bool* inside) {
+    constexpr float kW = (float)(kWaveTile - 1), kH = (float)(kWaveTileH - 1);
     if (is_tri) {
-        const float xl = x0 - k.a.x, xh = (x0 + 15.0f) - k.a.x;
-        const float yl = y0 - k.a.y, yh = (y0 + 15.0f) - k.a.y;
+        const float xl = x0 - k.a.x, xh = (x0 + kW) - k.a.x;
+        const float yl = y0 - k.a.y, yh = (y0 + kH) - k.a.y;
         const float u1 = k.a.z * xl, u2 = k.a.z * xh, u3 = k.a.w * yl, u4 = k.a.w * yh;
         const float v1 = k.b.x * xl, v2 = k.b.x * xh, v3 = k.b.y * yl, v4 = k.b.y * yh;
         const float umin = fminf(u1, u2) + fminf(u3, u4), umax = fmaxf(u1, u2) + fmaxf(u3, u4);
@@ -538,8 +561,8 @@ __device__ __forceinline__ void classify(const Cls& k, bool is_tri, float x0, fl
         *inside = umin > g && umax < 1.0f - g && vmin > g && vmax < 1.0f - g &&
                   umax + vmax < 1.0f - g;
     } else {
-        const float dx = fmaxf(fmaxf(x0 - k.a.x, k.a.x - (x0 + 15.0f)), 0.0f);
-        const float dy = fmaxf(fmaxf(y0 - k.a.y, k.a.y - (y0 + 15.0f)), 0.0f);
+        const float dx = fmaxf(fmaxf(x0 - k.a.x, k.a.x - (x0 + kW)), 0.0f);
+        const float dy = fmaxf(fmaxf(y0 - k.a.y, k.a.y - (y0 + kH)), 0.0f);
         *keep = !(dx * dx + dy * dy > k.a.z);
         *inside = false;
     }
@@ -577,9 +600,9 @@ __global__ void __launch_bounds__(kThreads) trace_kernel(
     const int bin_x = (bin % n_bins_x) * kBinW;
     const int bin_y = (bin / n_bins_x) * kBinH;  // relative to row_begin
     const int tile_x = bin_x + (wave & 1) * kWaveTile;
-    const int tile_y = row_begin + bin_y + (wave >> 1) * kWaveTile;
-    const int x = tile_x + (lane & 15);
-    const int y0 = tile_y + (lane >> 4);
+    const int tile_y = row_begin + bin_y + (wave >> 1) * kWaveTileH;
+    const int x = tile_x + (lane % kWaveTile);
+    const int y0 = tile_y + (lane / kWaveTile);
     const int n_tri = 12 * scene.n_cubes;
 
     if (kMode == 0 && *nonfinite_flag == gen) {
@@ -587,7 +610,7 @@ __global__ void __launch_bounds__(kThreads) trace_kernel(
         // assume finite values, so run the reference algorithm verbatim.
 #pragma unroll 1
         for (int j = 0; j < kRowsPerLane; ++j) {
-            const int y = y0 + 4 * j;
+            const int y = y0 + kLaneRows * j;
             if (x >= width || y >= row_end) continue;
             const int4v p =
                 collide_generic(scene, make_float4((float)x, (float)y, 0.0f, 1.0f), dir);
@@ -604,12 +627,12 @@ __global__ void __launch_bounds__(kThreads) trace_kernel(
     for (int j = 0; j < kRowsPerLane; ++j) {
         closest[j] = kFar;
         hit[j] = -1;
-        py[j] = (double)(y0 + 4 * j);
-        pyf[j] = (float)(y0 + 4 * j);
+        py[j] = (double)(y0 + kLaneRows * j);
+        pyf[j] = (float)(y0 + kLaneRows * j);
     }
     const double px = (double)x;
     const float pxf = (float)x;
-    const int tx1 = tile_x + kWaveTile - 1, ty1 = tile_y + kWaveTile - 1;
+    const int tx1 = tile_x + kWaveTile - 1, ty1 = tile_y + kWaveTileH - 1;
 
     const int cb = (bin_y / kCoarse) * n_cx + bin_x / kCoarse;
     const int count = kMode == 1 ? 0 : counts[cb];
@@ -633,8 +656,12 @@ __global__ void __launch_bounds__(kThreads) trace_kernel(
                 const int4 b = s_box[e];
                 id = s_id[e];
                 if (b.x <= tx1 && b.z >= tile_x && b.y <= ty1 && b.w >= tile_y) {
+#if RT_TILECLS
                     kc = s_cls[e];
                     classify(kc, id < n_tri, (float)tile_x, (float)tile_y, &keep, &inside);
+#else
+                    keep = true;
+#endif
                 }
             }
             unsigned long long m = __ballot(keep);
@@ -647,11 +674,13 @@ __global__ void __launch_bounds__(kThreads) trace_kernel(
                     hit[0] = hit[0] > p ? hit[0] : -1;  // keep the walk alive
                     continue;
                 }
-                Cls k;
+                Cls k{};
+#if RT_PIXCLS
                 k.a = make_float4(readlane_f(kc.a.x, bit), readlane_f(kc.a.y, bit),
                                   readlane_f(kc.a.z, bit), readlane_f(kc.a.w, bit));
                 k.b = make_float4(readlane_f(kc.b.x, bit), readlane_f(kc.b.y, bit),
                                   readlane_f(kc.b.z, bit), 0.0f);
+#endif
                 test_primitive(p, (mi >> bit) & 1ull, k, n_tri, tri, sph, px, pxf, py, pyf,
                                closest, hit);
             }
@@ -660,11 +689,13 @@ __global__ void __launch_bounds__(kThreads) trace_kernel(
 
     // Shade + store.  A wave whose 256 pixels all missed (ballot) stores the
     // black pattern without touching the colour arrays.
-    const bool any_hit =
-        __ballot(hit[0] >= 0 || hit[1] >= 0 || hit[2] >= 0 || hit[3] >= 0) != 0ull;
+    bool lane_hit = false;
+#pragma unroll
+    for (int j = 0; j < kRowsPerLane; ++j) lane_hit |= hit[j] >= 0;
+    const bool any_hit = __ballot(lane_hit) != 0ull;
 #pragma unroll
     for (int j = 0; j < kRowsPerLane; ++j) {
-        const int y = y0 + 4 * j;
+        const int y = y0 + kLaneRows * j;
         int4v pix{0, 0, 0, 255};
         if (any_hit && hit[j] >= 0) {
             const float4 col = hit[j] < n_tri ? scene.cube_colours[hit[j] / 12]

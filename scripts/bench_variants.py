@@ -1,0 +1,92 @@
+"""A/B timing of librt_hip.so variants in ONE process, interleaved rounds
+(cdna_hip_programming.md §5.4 rule 24), on the bench's config-3 scene.
+Every variant's frame is checked bit-exact against the first variant's.
+
+    python scripts/bench_variants.py opencl-ray-tracer_amd/variants/librt_hip_*.so
+"""
+import argparse
+import ctypes
+import json
+import statistics
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+REPO = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(REPO))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("libs", nargs="+")
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--width", type=int, default=4096)
+    ap.add_argument("--height", type=int, default=4096)
+    ap.add_argument("--spheres", type=int, default=256)
+    ap.add_argument("--cubes", type=int, default=64)
+    ap.add_argument("--seed", type=int, default=3)
+    ap.add_argument("--k", type=float, default=None)
+    args = ap.parse_args()
+    import torch
+    import __graft_entry__
+    pkg = __graft_entry__.load_package()
+    w, h = args.width, args.height
+    k = args.k if args.k is not None else w / 640
+    scene = pkg.Scene.synthetic(w, h, args.spheres, args.cubes, seed=args.seed, k=k)
+    dev = torch.device("cuda:0")
+    t = {n: torch.from_numpy(np.ascontiguousarray(getattr(scene, n))).to(dev)
+         for n in ("sphere_origins", "sphere_radius", "sphere_colours", "cube_vertices",
+                   "cube_colours")}
+    sc = pkg._Scene(t["sphere_origins"].data_ptr(), t["sphere_radius"].data_ptr(),
+                    t["sphere_colours"].data_ptr(), scene.num_spheres,
+                    t["cube_vertices"].data_ptr(), t["cube_colours"].data_ptr(),
+                    scene.num_cubes, None, 0)
+    d = pkg.primary_ray_dir()
+    stream = torch.cuda.Stream(dev)
+    out = torch.empty((h, w, 4), dtype=torch.int32, device=dev)
+    libs = []
+    for path in args.libs:
+        lib = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
+        ctx = ctypes.c_void_p()
+        assert lib.rt_init(0, ctypes.byref(ctx)) == 0
+        lib.rt_render_device.argtypes = [ctypes.c_void_p, ctypes.POINTER(pkg._Scene),
+                                         ctypes.c_void_p, ctypes.c_void_p] + \
+            [ctypes.c_int32] * 6 + [ctypes.c_void_p, ctypes.c_void_p]
+        libs.append((Path(path).stem.replace("librt_hip_", ""), lib, ctx))
+
+    def run(lib, ctx, n):
+        for _ in range(n):
+            rc = lib.rt_render_device(ctx, ctypes.byref(sc), d.ctypes.data, None, w, h, 0, h, 0,
+                                      0, out.data_ptr(), stream.cuda_stream)
+            assert rc == 0
+
+    ref = None
+    for name, lib, ctx in libs:  # warmup + parity
+        run(lib, ctx, 3)
+        torch.cuda.synchronize()
+        frame = out.cpu()
+        if ref is None:
+            ref = frame
+        elif not torch.equal(frame, ref):
+            print(f"PARITY MISMATCH {name}: {(frame != ref).any(-1).sum().item()} px", flush=True)
+    times = {name: [] for name, _, _ in libs}
+    for r in range(args.rounds):
+        order = libs if r % 2 == 0 else libs[::-1]
+        for name, lib, ctx in order:
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            run(lib, ctx, args.steps)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            times[name].append(e0.elapsed_time(e1) / args.steps * 1e3)
+    res = {n: {"median_us": round(statistics.median(v), 2), "min_us": round(min(v), 2)}
+           for n, v in times.items()}
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
