@@ -268,6 +268,30 @@ __device__ __forceinline__ int cvt_i32(float f) {
     return (f >= -2147483648.0f && f < 2147483648.0f) ? (int)f : INT32_MIN;
 }
 
+// The same on the hot path: v_cvt_i32_f32 truncates and saturates (-inf and
+// everything below -2^31 -> INT32_MIN, NaN -> 0, >= 2^31 -> INT32_MAX); the
+// one compare maps NaN and >= 2^31 to x86's INT32_MIN.  Inline asm keeps the
+// hardware semantics (a C++ (int) of an out-of-range float is undefined).
+__device__ __forceinline__ int cvt_i32_fast(float f) {
+    int r;
+    asm volatile("v_cvt_i32_f32 %0, %1" : "=v"(r) : "v"(f));
+    return f < 2147483648.0f ? r : INT32_MIN;
+}
+
+// Correctly rounded x / 180.0f without the IEEE division sequence:
+// q0 = x * RN(1/180), q = fma(fma(-q0, 180, x), RN(1/180), q0) equals RN(x/180)
+// for every finite float with |x| >= 2^-100 (exhaustively checked on the host,
+// scripts/check_div180.c); smaller |x| takes the division.
+__device__ __forceinline__ float div180(float x) {
+    const float r = 1.0f / 180.0f;
+    const float q0 = x * r;
+    const float rem = __builtin_fmaf(-q0, 180.0f, x);
+    float q = __builtin_fmaf(rem, r, q0);
+    const bool tiny = !(__builtin_fabsf(x) >= 0x1p-100f);
+    if (__ballot(tiny)) q = tiny ? x / 180.0f : q;
+    return q;
+}
+
 // MainState.cpp:396-407 + :952-955 (or the Texture packing :1026-1036).
 __device__ __forceinline__ int4v shade(float closest, float4 colour) {
     if (closest == kFar) return int4v{0, 0, 0, 255};
@@ -275,6 +299,14 @@ __device__ __forceinline__ int4v shade(float closest, float4 colour) {
     const float scalar = 255.0f - (normalised * 255.0f);
     return int4v{cvt_i32(scalar * colour.x), cvt_i32(scalar * colour.y),
                  cvt_i32(scalar * colour.z), 255};
+}
+
+// Hot-path shade of a hit pixel (closest < 300000 always holds here).
+__device__ __forceinline__ int4v shade_hit(float closest, float4 colour) {
+    const float normalised = div180(closest - 0.0f);
+    const float scalar = 255.0f - (normalised * 255.0f);
+    return int4v{cvt_i32_fast(scalar * colour.x), cvt_i32_fast(scalar * colour.y),
+                 cvt_i32_fast(scalar * colour.z), 255};
 }
 
 __device__ __forceinline__ unsigned pack_rgba8(int4v p) {
@@ -384,7 +416,8 @@ __global__ void __launch_bounds__(kThreads) generic_kernel(
 __global__ void __launch_bounds__(kThreads) prep_kernel(
     SceneDev scene, float4 dir, int width, int row_begin, int row_end,
     TriRec* __restrict__ tri, SphRec* __restrict__ sph, int4* __restrict__ boxes,
-    Cls* __restrict__ cls, unsigned* __restrict__ nonfinite_flag, unsigned gen) {
+    Cls* __restrict__ cls, float4* __restrict__ colours, unsigned* __restrict__ nonfinite_flag,
+    unsigned gen) {
     const int n_tri = 12 * scene.n_cubes;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     Box b = empty_box();
@@ -394,6 +427,7 @@ __global__ void __launch_bounds__(kThreads) prep_kernel(
         const float4* v = scene.cube_vertices + 3 * i;
         const float4 a = v[0], bb = v[1], c = v[2];
         const float fa[3] = {a.x, a.y, a.z}, fb[3] = {bb.x, bb.y, bb.z}, fc[3] = {c.x, c.y, c.z};
+        if (i % 12 == 0) colours[i / 12] = scene.cube_colours[i / 12];
         TriRec r{};
         prep_triangle(fa, fb, fc, (double)dir.x, (double)dir.y, (double)dir.z, width, row_begin,
                       row_end, &r, &b, &k, &bad);
@@ -401,6 +435,7 @@ __global__ void __launch_bounds__(kThreads) prep_kernel(
     } else if (i < n_tri + scene.n_spheres) {
         const int s = i - n_tri;
         const float4 o = scene.sphere_origins[s];
+        colours[scene.n_cubes + s] = scene.sphere_colours[s];
         const float fo[4] = {o.x, o.y, o.z, o.w};
         SphRec r{};
         prep_sphere(fo, scene.sphere_radius[s], dir.x, dir.y, dir.z, dir.w, width, row_begin,
@@ -450,8 +485,8 @@ __global__ void __launch_bounds__(kThreads) coarse_kernel(
 // the per-triangle constants (see TriRec); `inside` (wave-uniform) means the
 // tile classifier proved every pixel of the tile passes the u/v tests, so
 // only the exact t is computed.  Spheres: :300-327 on SphRec.
-__device__ __forceinline__ void test_primitive(int p, bool inside, const Cls& k, int n_tri,
-                                               const TriRec* __restrict__ tri,
+__device__ __forceinline__ void test_primitive(int p, int slot, bool inside, const Cls& k,
+                                               int n_tri, const TriRec* __restrict__ tri,
                                                const SphRec* __restrict__ sph, double px,
                                                float pxf, const double* py, const float* pyf,
                                                float* closest, int* hit) {
@@ -469,7 +504,7 @@ __device__ __forceinline__ void test_primitive(int p, bool inside, const Cls& k,
                 const float tf = (float)t;
                 if (tf < closest[j]) {
                     closest[j] = tf;
-                    hit[j] = p;
+                    hit[j] = slot;
                 }
             }
             return;
@@ -513,7 +548,7 @@ __device__ __forceinline__ void test_primitive(int p, bool inside, const Cls& k,
                 const float tf = (float)t;
                 if (tf < closest[j]) {
                     closest[j] = tf;
-                    hit[j] = p;
+                    hit[j] = slot;
                 }
             }
         }
@@ -531,7 +566,7 @@ __device__ __forceinline__ void test_primitive(int p, bool inside, const Cls& k,
                 const float t0 = s.tca - thc;
                 if (t0 != 0.0f && t0 < closest[j]) {
                     closest[j] = t0;
-                    hit[j] = p;
+                    hit[j] = slot;
                 }
             }
         }
@@ -576,24 +611,27 @@ __device__ __forceinline__ void store_pixel(void* __restrict__ out, int out_form
         reinterpret_cast<unsigned*>(out)[idx] = pack_rgba8(pix);
 }
 
-// One workgroup per 32x32 bin, one 16x16 tile per wave, kRowsPerLane pixels
-// per lane.  The parent coarse bin's candidate list (ids + boxes) is staged
-// in LDS once per workgroup; each wave filters it against its own tile with
-// one ballot per 64 entries and walks the surviving candidates in order
-// (v_readlane -> scalar record loads -> per-lane exact tests).
+// One workgroup per bin (2x2 wave tiles), kRowsPerLane pixels per lane.
+// The parent coarse bin's candidate list (ids, boxes, classifiers) is staged
+// in LDS once per workgroup; each wave filters it against its own tile (one
+// ballot per 64 entries, compacted in order into a per-wave LDS list with the
+// tile classification in bit 31), then walks that list with one flat uniform
+// loop: scalar record loads -> per-lane exact tests.
 // kMode is a diagnostics ablation (rt_debug_set_trace_mode): 0 = the real
 // kernel, 1 = stores only (the store floor of this exact pattern), 2 = stage
 // and filter candidates but skip the per-pixel tests.
 template <int kMode>
 __global__ void __launch_bounds__(kThreads) trace_kernel(
     SceneDev scene, const TriRec* __restrict__ tri, const SphRec* __restrict__ sph,
-    const int4* __restrict__ boxes, const Cls* __restrict__ cls, const int* __restrict__ counts,
+    const int4* __restrict__ boxes, const Cls* __restrict__ cls,
+    const float4* __restrict__ colours, const int* __restrict__ counts,
     const int* __restrict__ lists, int cap, const unsigned* __restrict__ nonfinite_flag,
     unsigned gen, float4 dir, int width, int row_begin, int row_end, int n_bins_x, int n_cx,
     int out_format, void* __restrict__ out) {
     __shared__ int s_id[kStage];
     __shared__ int4 s_box[kStage];
     __shared__ Cls s_cls[kStage];
+    __shared__ int s_wlist[kThreads / 64][kStage];
     const int bin = blockIdx.x;
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
@@ -620,7 +658,7 @@ __global__ void __launch_bounds__(kThreads) trace_kernel(
     }
 
     float closest[kRowsPerLane];
-    int hit[kRowsPerLane];
+    int hit[kRowsPerLane];  // colour slot of the closest primitive, -1 = none
     double py[kRowsPerLane];
     float pyf[kRowsPerLane];
 #pragma unroll
@@ -637,6 +675,7 @@ __global__ void __launch_bounds__(kThreads) trace_kernel(
     const int cb = (bin_y / kCoarse) * n_cx + bin_x / kCoarse;
     const int count = kMode == 1 ? 0 : counts[cb];
     const int* __restrict__ list = lists + (int64_t)cb * cap;
+    int* wlist = s_wlist[wave];
     for (int s0 = 0; s0 < count; s0 += kStage) {
         const int n = min(kStage, count - s0);
         if (s0 > 0) __syncthreads();  // previous stage fully consumed
@@ -647,48 +686,49 @@ __global__ void __launch_bounds__(kThreads) trace_kernel(
             s_cls[i] = cls[id];
         }
         __syncthreads();
+        // filter: this wave's candidates, in order, into wlist
+        int wn = 0;
         for (int c = 0; c < n; c += 64) {
             const int e = c + lane;
             bool keep = false, inside = false;
             int id = 0;
-            Cls kc{};
             if (e < n) {
                 const int4 b = s_box[e];
                 id = s_id[e];
                 if (b.x <= tx1 && b.z >= tile_x && b.y <= ty1 && b.w >= tile_y) {
 #if RT_TILECLS
-                    kc = s_cls[e];
-                    classify(kc, id < n_tri, (float)tile_x, (float)tile_y, &keep, &inside);
+                    classify(s_cls[e], id < n_tri, (float)tile_x, (float)tile_y, &keep, &inside);
 #else
                     keep = true;
 #endif
                 }
             }
-            unsigned long long m = __ballot(keep);
-            const unsigned long long mi = __ballot(keep && inside);
-            while (m) {
-                const int bit = __builtin_ctzll(m);
-                m &= m - 1;
-                const int p = __builtin_amdgcn_readlane(id, bit);
-                if (kMode == 2) {
-                    hit[0] = hit[0] > p ? hit[0] : -1;  // keep the walk alive
-                    continue;
-                }
-                Cls k{};
-#if RT_PIXCLS
-                k.a = make_float4(readlane_f(kc.a.x, bit), readlane_f(kc.a.y, bit),
-                                  readlane_f(kc.a.z, bit), readlane_f(kc.a.w, bit));
-                k.b = make_float4(readlane_f(kc.b.x, bit), readlane_f(kc.b.y, bit),
-                                  readlane_f(kc.b.z, bit), 0.0f);
-#endif
-                test_primitive(p, (mi >> bit) & 1ull, k, n_tri, tri, sph, px, pxf, py, pyf,
-                               closest, hit);
+            const unsigned long long m = __ballot(keep);
+            if (keep) {
+                const unsigned below = __builtin_amdgcn_mbcnt_hi(
+                    (unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+                wlist[wn + (int)below] = id | (inside ? (int)0x80000000u : 0);
             }
+            wn += __popcll(m);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (int i = 0; i < wn; ++i) {
+            const int v = __builtin_amdgcn_readfirstlane(wlist[i]);
+            const int p = v & 0x7fffffff;
+            if (kMode == 2) {
+                hit[0] = hit[0] > p ? hit[0] : -1;  // keep the walk alive
+                continue;
+            }
+            const int slot = p < n_tri ? p / 12 : scene.n_cubes + (p - n_tri);
+            test_primitive(p, slot, v < 0, Cls{}, n_tri, tri, sph, px, pxf, py, pyf, closest,
+                           hit);
         }
     }
 
-    // Shade + store.  A wave whose 256 pixels all missed (ballot) stores the
-    // black pattern without touching the colour arrays.
+    // Shade + store.  A wave whose pixels all missed (ballot) stores the
+    // black pattern without touching the colour table.
     bool lane_hit = false;
 #pragma unroll
     for (int j = 0; j < kRowsPerLane; ++j) lane_hit |= hit[j] >= 0;
@@ -697,12 +737,9 @@ __global__ void __launch_bounds__(kThreads) trace_kernel(
     for (int j = 0; j < kRowsPerLane; ++j) {
         const int y = y0 + kLaneRows * j;
         int4v pix{0, 0, 0, 255};
-        if (any_hit && hit[j] >= 0) {
-            const float4 col = hit[j] < n_tri ? scene.cube_colours[hit[j] / 12]
-                                              : scene.sphere_colours[hit[j] - n_tri];
-            pix = shade(closest[j], col);
-        }
-        if (x < width && y < row_end) store_pixel(out, out_format, (int64_t)(y - row_begin) * width + x, pix);
+        if (any_hit && hit[j] >= 0) pix = shade_hit(closest[j], colours[hit[j]]);
+        if (x < width && y < row_end)
+            store_pixel(out, out_format, (int64_t)(y - row_begin) * width + x, pix);
     }
 }
 
@@ -840,7 +877,9 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
     const size_t sph_off = align_up(sizeof(TriRec) * (size_t)n_tri, 256);
     const size_t box_off = sph_off + align_up(sizeof(SphRec) * (size_t)s->num_spheres, 256);
     const size_t cls_off = box_off + align_up(sizeof(int4) * (size_t)n_prims, 256);
-    const size_t cnt_off = cls_off + align_up(sizeof(Cls) * (size_t)n_prims, 256);
+    const size_t col_off = cls_off + align_up(sizeof(Cls) * (size_t)n_prims, 256);
+    const size_t cnt_off =
+        col_off + align_up(sizeof(float4) * (size_t)(s->num_cubes + s->num_spheres), 256);
     const size_t rec_need = cnt_off + align_up(sizeof(int) * (size_t)n_coarse, 256);
     int rc = ensure(&ctx->rec_buf, &ctx->rec_cap, rec_need);
     if (rc) return rc;
@@ -852,6 +891,7 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
     SphRec* sph = reinterpret_cast<SphRec*>(base + sph_off);
     int4* boxes = reinterpret_cast<int4*>(base + box_off);
     Cls* clsv = reinterpret_cast<Cls*>(base + cls_off);
+    float4* colours = reinterpret_cast<float4*>(base + col_off);
     int* counts = reinterpret_cast<int*>(base + cnt_off);
     int* lists = static_cast<int*>(ctx->list_buf);
     // generation-stamped non-finite flag: no per-launch memset needed
@@ -862,7 +902,8 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
 
     if (n_prims > 0) {
         prep_kernel<<<dim3((n_prims + kThreads - 1) / kThreads), dim3(kThreads), 0, stream>>>(
-            sd, dir, width, row_begin, row_end, tri, sph, boxes, clsv, ctx->flag, ctx->gen);
+            sd, dir, width, row_begin, row_end, tri, sph, boxes, clsv, colours, ctx->flag,
+            ctx->gen);
         HIP_TRY(hipGetLastError());
     }
     if (pe) HIP_TRY(hipEventRecord(pe[1], stream));
@@ -873,7 +914,8 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
     auto kern = ctx->trace_mode == 1 ? trace_kernel<1>
               : ctx->trace_mode == 2 ? trace_kernel<2> : trace_kernel<0>;
     kern<<<dim3((unsigned)n_bins), dim3(kThreads), 0, stream>>>(
-        sd, tri, sph, boxes, clsv, counts, lists, cap, ctx->flag, ctx->gen, dir, width, row_begin,
+        sd, tri, sph, boxes, clsv, colours, counts, lists, cap, ctx->flag, ctx->gen, dir, width,
+        row_begin,
         row_end, n_bins_x, n_cx, fmt, out);
     HIP_TRY(hipGetLastError());
     if (pe) HIP_TRY(hipEventRecord(pe[3], stream));
