@@ -619,7 +619,9 @@ __device__ __forceinline__ void store_pixel(void* __restrict__ out, int out_form
 // loop: scalar record loads -> per-lane exact tests.
 // kMode is a diagnostics ablation (rt_debug_set_trace_mode): 0 = the real
 // kernel, 1 = stores only (the store floor of this exact pattern), 2 = stage
-// and filter candidates but skip the per-pixel tests.
+// and filter candidates but skip the per-pixel tests, 3 = everything but the
+// framebuffer stores, 4 = per-pixel tests without the per-candidate record
+// loads (wrong pixels; timing only).
 template <int kMode>
 __global__ void __launch_bounds__(kThreads) trace_kernel(
     SceneDev scene, const TriRec* __restrict__ tri, const SphRec* __restrict__ sph,
@@ -722,7 +724,9 @@ __global__ void __launch_bounds__(kThreads) trace_kernel(
                 continue;
             }
             const int slot = p < n_tri ? p / 12 : scene.n_cubes + (p - n_tri);
-            test_primitive(p, slot, v < 0, Cls{}, n_tri, tri, sph, px, pxf, py, pyf, closest,
+            // kMode 4: same tests on record 0 / sphere 0 (no dependent record loads)
+            const int pr = kMode == 4 ? (p < n_tri ? 0 : n_tri) : p;
+            test_primitive(pr, slot, v < 0, Cls{}, n_tri, tri, sph, px, pxf, py, pyf, closest,
                            hit);
         }
     }
@@ -738,7 +742,9 @@ __global__ void __launch_bounds__(kThreads) trace_kernel(
         const int y = y0 + kLaneRows * j;
         int4v pix{0, 0, 0, 255};
         if (any_hit && hit[j] >= 0) pix = shade_hit(closest[j], colours[hit[j]]);
-        if (x < width && y < row_end)
+        // kMode 3: everything but the stores (a store the compiler cannot drop)
+        const bool store = kMode != 3 || pix.x == 0x7fffffff;
+        if (x < width && y < row_end && store)
             store_pixel(out, out_format, (int64_t)(y - row_begin) * width + x, pix);
     }
 }
@@ -912,7 +918,9 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
     HIP_TRY(hipGetLastError());
     if (pe) HIP_TRY(hipEventRecord(pe[2], stream));
     auto kern = ctx->trace_mode == 1 ? trace_kernel<1>
-              : ctx->trace_mode == 2 ? trace_kernel<2> : trace_kernel<0>;
+              : ctx->trace_mode == 2 ? trace_kernel<2>
+              : ctx->trace_mode == 3 ? trace_kernel<3>
+              : ctx->trace_mode == 4 ? trace_kernel<4> : trace_kernel<0>;
     kern<<<dim3((unsigned)n_bins), dim3(kThreads), 0, stream>>>(
         sd, tri, sph, boxes, clsv, colours, counts, lists, cap, ctx->flag, ctx->gen, dir, width,
         row_begin,
@@ -1150,7 +1158,7 @@ int rt_debug_triangle_box(const float v0[3], const float v1[3], const float v2[3
 
 // Diagnostics: select a trace-kernel ablation (0 = normal).
 int rt_debug_set_trace_mode(rt_ctx* ctx, int mode) {
-    if (!ctx || mode < 0 || mode > 2) return RT_ERR_INVALID_ARG;
+    if (!ctx || mode < 0 || mode > 4) return RT_ERR_INVALID_ARG;
     ctx->trace_mode = mode;
     return RT_OK;
 }
