@@ -55,10 +55,18 @@ constexpr int kWaveTile = RT_TILE_W;                       // wave tile width
 constexpr int kRowsPerLane = RT_ROWS;
 constexpr int kLaneRows = 64 / RT_TILE_W;                  // lane rows per pass
 constexpr int kWaveTileH = kLaneRows * RT_ROWS;            // wave tile height
-constexpr int kBinW = 2 * kWaveTile;  // bin = workgroup tile (2x2 wave tiles)
-constexpr int kBinH = 2 * kWaveTileH;
+#ifndef RT_WAVES_X
+#define RT_WAVES_X 2              // wave tiles per trace workgroup, x
+#endif
+#ifndef RT_WAVES_Y
+#define RT_WAVES_Y 2              // wave tiles per trace workgroup, y
+#endif
+constexpr int kWavesX = RT_WAVES_X, kWavesY = RT_WAVES_Y;
+constexpr int kTraceThreads = 64 * kWavesX * kWavesY;
+constexpr int kBinW = kWavesX * kWaveTile;  // bin = trace workgroup tile
+constexpr int kBinH = kWavesY * kWaveTileH;
 constexpr int kCoarse = 64;       // coarse bin (candidate list) edge, pixels
-constexpr int kStage = 128;       // candidate entries staged in LDS per pass
+constexpr int kStage = 256;       // candidate entries staged in LDS per pass
 static_assert(64 % kBinW == 0 && 64 % kBinH == 0, "bins must tile a coarse bin");
 constexpr int kThreads = 256;
 constexpr double kEpsilon = 0.000001;      // MainState.cpp:15
@@ -440,10 +448,7 @@ __global__ void __launch_bounds__(kThreads) prep_kernel(
         SphRec r{};
         prep_sphere(fo, scene.sphere_radius[s], dir.x, dir.y, dir.z, dir.w, width, row_begin,
                     row_end, &r, &b, &k, &bad);
-        TriRec slot{};
-        __builtin_memcpy(&slot, &r, sizeof r);
-        tri[i] = slot;  // one 128-B record slot per primitive
-        (void)sph;
+        sph[s] = r;
     } else {
         return;
     }
@@ -488,11 +493,13 @@ __global__ void __launch_bounds__(kThreads) coarse_kernel(
 // the per-triangle constants (see TriRec); `inside` (wave-uniform) means the
 // tile classifier proved every pixel of the tile passes the u/v tests, so
 // only the exact t is computed.  Spheres: :300-327 on SphRec.
-__device__ __forceinline__ void test_primitive(bool is_tri, int slot, bool inside, const Cls& k,
-                                               const TriRec& r, double px, float pxf,
-                                               const double* py, const float* pyf,
+__device__ __forceinline__ void test_primitive(int p, int slot, bool inside, const Cls& k,
+                                               int n_tri, const TriRec* __restrict__ tri,
+                                               const SphRec* __restrict__ sph, double px,
+                                               float pxf, const double* py, const float* pyf,
                                                float* closest, int* hit) {
-    if (is_tri) {
+    if (p < n_tri) {
+        const TriRec r = tri[p];
         const double tx = px - r.v0x;
         if (inside) {
 #pragma unroll
@@ -554,8 +561,7 @@ __device__ __forceinline__ void test_primitive(bool is_tri, int slot, bool insid
             }
         }
     } else {
-        SphRec s;
-        __builtin_memcpy(&s, &r, sizeof s);  // spheres share the 128-B record slots
+        const SphRec s = sph[p - n_tri];
         const float lx = s.cx - pxf;
         const float lx2 = lx * lx;
 #pragma unroll
@@ -625,7 +631,7 @@ __device__ __forceinline__ void store_pixel(void* __restrict__ out, int out_form
 // framebuffer stores, 4 = per-pixel tests without the per-candidate record
 // loads (wrong pixels; timing only).
 template <int kMode>
-__global__ void __launch_bounds__(kThreads) trace_kernel(
+__global__ void __launch_bounds__(kTraceThreads) trace_kernel(
     SceneDev scene, const TriRec* __restrict__ tri, const SphRec* __restrict__ sph,
     const int4* __restrict__ boxes, const Cls* __restrict__ cls,
     const float4* __restrict__ colours, const int* __restrict__ counts,
@@ -635,15 +641,14 @@ __global__ void __launch_bounds__(kThreads) trace_kernel(
     __shared__ int s_id[kStage];
     __shared__ int4 s_box[kStage];
     __shared__ Cls s_cls[kStage];
-    __shared__ TriRec s_rec[kStage];
-    __shared__ int s_wlist[kThreads / 64][kStage];
+    __shared__ int s_wlist[kTraceThreads / 64][kStage];
     const int bin = blockIdx.x;
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
     const int bin_x = (bin % n_bins_x) * kBinW;
     const int bin_y = (bin / n_bins_x) * kBinH;  // relative to row_begin
-    const int tile_x = bin_x + (wave & 1) * kWaveTile;
-    const int tile_y = row_begin + bin_y + (wave >> 1) * kWaveTileH;
+    const int tile_x = bin_x + (wave % kWavesX) * kWaveTile;
+    const int tile_y = row_begin + bin_y + (wave / kWavesX) * kWaveTileH;
     const int x = tile_x + (lane % kWaveTile);
     const int y0 = tile_y + (lane / kWaveTile);
     const int n_tri = 12 * scene.n_cubes;
@@ -684,17 +689,11 @@ __global__ void __launch_bounds__(kThreads) trace_kernel(
     for (int s0 = 0; s0 < count; s0 += kStage) {
         const int n = min(kStage, count - s0);
         if (s0 > 0) __syncthreads();  // previous stage fully consumed
-        for (int i = threadIdx.x; i < n; i += kThreads) {
+        for (int i = threadIdx.x; i < n; i += kTraceThreads) {
             const int id = list[s0 + i];
             s_id[i] = id;
             s_box[i] = boxes[id];
             s_cls[i] = cls[id];
-        }
-        // the candidates' 128-B records: 8 lanes per record, 16 B each
-        for (int i = threadIdx.x; i < n * 8; i += kThreads) {
-            const int id = list[s0 + (i >> 3)];
-            reinterpret_cast<float4*>(s_rec)[i] =
-                reinterpret_cast<const float4*>(tri + id)[i & 7];
         }
         __syncthreads();
         // filter: this wave's candidates, in order, into wlist
@@ -718,28 +717,25 @@ __global__ void __launch_bounds__(kThreads) trace_kernel(
             if (keep) {
                 const unsigned below = __builtin_amdgcn_mbcnt_hi(
                     (unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-                wlist[wn + (int)below] = e | (inside ? (int)0x80000000u : 0);
+                wlist[wn + (int)below] = id | (inside ? (int)0x80000000u : 0);
             }
             wn += __popcll(m);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (kMode == 2) {
-            for (int i = 0; i < wn; ++i) {
-                const int p = __builtin_amdgcn_readfirstlane(wlist[i]) & 0x7fffffff;
-                hit[0] = hit[0] > p ? hit[0] : -1;  // keep the walk alive
-            }
-            continue;
-        }
-        // Walk the wave's list; records come from LDS (broadcast reads).
         for (int i = 0; i < wn; ++i) {
             const int v = __builtin_amdgcn_readfirstlane(wlist[i]);
-            const int e = v & 0x7fffffff;
-            const int p = __builtin_amdgcn_readfirstlane(s_id[e]);
+            const int p = v & 0x7fffffff;
+            if (kMode == 2) {
+                hit[0] = hit[0] > p ? hit[0] : -1;  // keep the walk alive
+                continue;
+            }
             const int slot = p < n_tri ? p / 12 : scene.n_cubes + (p - n_tri);
-            const TriRec r = s_rec[kMode == 4 ? 0 : e];
-            test_primitive(p < n_tri, slot, v < 0, Cls{}, r, px, pxf, py, pyf, closest, hit);
+            // kMode 4: same tests on record 0 / sphere 0 (no dependent record loads)
+            const int pr = kMode == 4 ? (p < n_tri ? 0 : n_tri) : p;
+            test_primitive(pr, slot, v < 0, Cls{}, n_tri, tri, sph, px, pxf, py, pyf, closest,
+                           hit);
         }
     }
 
@@ -892,7 +888,7 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
     const int cap = n_prims > 0 ? n_prims : 1;
 
     const size_t tri_off = 0;
-    const size_t sph_off = align_up(sizeof(TriRec) * (size_t)n_prims, 256);
+    const size_t sph_off = align_up(sizeof(TriRec) * (size_t)n_tri, 256);
     const size_t box_off = sph_off + align_up(sizeof(SphRec) * (size_t)s->num_spheres, 256);
     const size_t cls_off = box_off + align_up(sizeof(int4) * (size_t)n_prims, 256);
     const size_t col_off = cls_off + align_up(sizeof(Cls) * (size_t)n_prims, 256);
@@ -933,7 +929,7 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
               : ctx->trace_mode == 2 ? trace_kernel<2>
               : ctx->trace_mode == 3 ? trace_kernel<3>
               : ctx->trace_mode == 4 ? trace_kernel<4> : trace_kernel<0>;
-    kern<<<dim3((unsigned)n_bins), dim3(kThreads), 0, stream>>>(
+    kern<<<dim3((unsigned)n_bins), dim3(kTraceThreads), 0, stream>>>(
         sd, tri, sph, boxes, clsv, colours, counts, lists, cap, ctx->flag, ctx->gen, dir, width,
         row_begin,
         row_end, n_bins_x, n_cx, fmt, out);
