@@ -48,6 +48,9 @@ namespace {
 #ifndef RT_TILECLS
 #define RT_TILECLS 1              // per-tile plane classification of candidates
 #endif
+#ifndef RT_STAMPS
+#define RT_STAMPS 0               // diagnostics build: per-phase s_memtime sums
+#endif
 #ifndef RT_PIXCLS
 #define RT_PIXCLS 0               // per-pixel fp32 pre-classification
 #endif
@@ -619,6 +622,21 @@ __device__ __forceinline__ void store_pixel(void* __restrict__ out, int out_form
         reinterpret_cast<unsigned*>(out)[idx] = pack_rgba8(pix);
 }
 
+#if RT_STAMPS
+// Diagnostics only (never in the shipped build): per-phase wave-cycle sums.
+// [0] stage+barrier [1] filter [2] walk [3] shade [4] store issue [5] waves
+// [6] triangle candidates [7] of which tile-inside [8] sphere candidates
+__device__ unsigned long long g_stamps[16];
+#define STAMP(t)                                                                   \
+    do {                                                                           \
+        __builtin_amdgcn_sched_barrier(0);                                         \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory"); \
+        __builtin_amdgcn_sched_barrier(0);                                         \
+    } while (0)
+#else
+#define STAMP(t) do { } while (0)
+#endif
+
 // One workgroup per bin (2x2 wave tiles), kRowsPerLane pixels per lane.
 // The parent coarse bin's candidate list (ids, boxes, classifiers) is staged
 // in LDS once per workgroup; each wave filters it against its own tile (one
@@ -682,6 +700,10 @@ __global__ void __launch_bounds__(kTraceThreads) trace_kernel(
     const float pxf = (float)x;
     const int tx1 = tile_x + kWaveTile - 1, ty1 = tile_y + kWaveTileH - 1;
 
+    unsigned long long st[6] = {0, 0, 0, 0, 0, 0}, ta = 0, tb = 0;
+    unsigned long long n_ct = 0, n_ci = 0, n_cs = 0;
+    (void)st; (void)ta; (void)tb; (void)n_ct; (void)n_ci; (void)n_cs;
+    STAMP(ta);
     const int cb = (bin_y / kCoarse) * n_cx + bin_x / kCoarse;
     const int count = kMode == 1 ? 0 : counts[cb];
     const int* __restrict__ list = lists + (int64_t)cb * cap;
@@ -696,6 +718,11 @@ __global__ void __launch_bounds__(kTraceThreads) trace_kernel(
             s_cls[i] = cls[id];
         }
         __syncthreads();
+        STAMP(tb);
+#if RT_STAMPS
+        st[0] += tb - ta;
+        ta = tb;
+#endif
         // filter: this wave's candidates, in order, into wlist
         int wn = 0;
         for (int c = 0; c < n; c += 64) {
@@ -724,6 +751,11 @@ __global__ void __launch_bounds__(kTraceThreads) trace_kernel(
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        STAMP(tb);
+#if RT_STAMPS
+        st[1] += tb - ta;
+        ta = tb;
+#endif
         for (int i = 0; i < wn; ++i) {
             const int v = __builtin_amdgcn_readfirstlane(wlist[i]);
             const int p = v & 0x7fffffff;
@@ -731,12 +763,22 @@ __global__ void __launch_bounds__(kTraceThreads) trace_kernel(
                 hit[0] = hit[0] > p ? hit[0] : -1;  // keep the walk alive
                 continue;
             }
+#if RT_STAMPS
+            n_ct += p < n_tri;
+            n_ci += p < n_tri && v < 0;
+            n_cs += p >= n_tri;
+#endif
             const int slot = p < n_tri ? p / 12 : scene.n_cubes + (p - n_tri);
             // kMode 4: same tests on record 0 / sphere 0 (no dependent record loads)
             const int pr = kMode == 4 ? (p < n_tri ? 0 : n_tri) : p;
             test_primitive(pr, slot, v < 0, Cls{}, n_tri, tri, sph, px, pxf, py, pyf, closest,
                            hit);
         }
+        STAMP(tb);
+#if RT_STAMPS
+        st[2] += tb - ta;
+        ta = tb;
+#endif
     }
 
     // Shade + store.  A wave whose pixels all missed (ballot) stores the
@@ -745,16 +787,39 @@ __global__ void __launch_bounds__(kTraceThreads) trace_kernel(
 #pragma unroll
     for (int j = 0; j < kRowsPerLane; ++j) lane_hit |= hit[j] >= 0;
     const bool any_hit = __ballot(lane_hit) != 0ull;
+    int4v pix[kRowsPerLane];
+#pragma unroll
+    for (int j = 0; j < kRowsPerLane; ++j) {
+        pix[j] = int4v{0, 0, 0, 255};
+        if (any_hit && hit[j] >= 0) pix[j] = shade_hit(closest[j], colours[hit[j]]);
+    }
+#if RT_STAMPS
+    asm volatile("" ::"v"(pix[0].x), "v"(pix[kRowsPerLane - 1].z));
+#endif
+    STAMP(tb);
+#if RT_STAMPS
+    st[3] += tb - ta;
+    ta = tb;
+#endif
 #pragma unroll
     for (int j = 0; j < kRowsPerLane; ++j) {
         const int y = y0 + kLaneRows * j;
-        int4v pix{0, 0, 0, 255};
-        if (any_hit && hit[j] >= 0) pix = shade_hit(closest[j], colours[hit[j]]);
         // kMode 3: everything but the stores (a store the compiler cannot drop)
-        const bool store = kMode != 3 || pix.x == 0x7fffffff;
+        const bool store = kMode != 3 || pix[j].x == 0x7fffffff;
         if (x < width && y < row_end && store)
-            store_pixel(out, out_format, (int64_t)(y - row_begin) * width + x, pix);
+            store_pixel(out, out_format, (int64_t)(y - row_begin) * width + x, pix[j]);
     }
+    STAMP(tb);
+#if RT_STAMPS
+    st[4] += tb - ta;
+    if (lane == 0) {
+        for (int k = 0; k < 5; ++k) atomicAdd(&g_stamps[k], st[k]);
+        atomicAdd(&g_stamps[5], 1ull);
+        atomicAdd(&g_stamps[6], n_ct);
+        atomicAdd(&g_stamps[7], n_ci);
+        atomicAdd(&g_stamps[8], n_cs);
+    }
+#endif
 }
 
 // fp32 self-test: the device's sqrtf and '/' must be correctly rounded.
@@ -1162,6 +1227,22 @@ int rt_debug_triangle_box(const float v0[3], const float v1[3], const float v2[3
     box_out[0] = b.x0; box_out[1] = b.y0; box_out[2] = b.x1; box_out[3] = b.y1;
     if (cls_out) std::memcpy(cls_out, &k, sizeof k);
     return ok ? 1 : 0;
+}
+
+// Diagnostics: read and reset the stamp sums of an RT_STAMPS build (returns
+// RT_ERR_UNSUPPORTED otherwise).
+int rt_debug_read_stamps(rt_ctx* ctx, unsigned long long out[16]) {
+    if (!ctx || !out) return RT_ERR_INVALID_ARG;
+#if RT_STAMPS
+    HIP_TRY(hipSetDevice(ctx->device));
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 16));
+    unsigned long long zero[16] = {};
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), zero, sizeof zero));
+    return RT_OK;
+#else
+    return RT_ERR_UNSUPPORTED;
+#endif
 }
 
 // Diagnostics: select a trace-kernel ablation (0 = normal).
