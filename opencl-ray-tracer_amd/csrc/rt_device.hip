@@ -626,7 +626,8 @@ __device__ __forceinline__ void store_pixel(void* __restrict__ out, int out_form
 // Diagnostics only (never in the shipped build): per-phase wave-cycle sums.
 // [0] stage+barrier [1] filter [2] walk [3] shade [4] store issue [5] waves
 // [6] triangle candidates [7] of which tile-inside [8] sphere candidates
-__device__ unsigned long long g_stamps[16];
+constexpr int kStampWaves = 1 << 17;  // per-wave slots of one launch
+__device__ unsigned long long g_stamps[kStampWaves * 8];
 #define STAMP(t)                                                                   \
     do {                                                                           \
         __builtin_amdgcn_sched_barrier(0);                                         \
@@ -812,12 +813,13 @@ __global__ void __launch_bounds__(kTraceThreads) trace_kernel(
     STAMP(tb);
 #if RT_STAMPS
     st[4] += tb - ta;
-    if (lane == 0) {
-        for (int k = 0; k < 5; ++k) atomicAdd(&g_stamps[k], st[k]);
-        atomicAdd(&g_stamps[5], 1ull);
-        atomicAdd(&g_stamps[6], n_ct);
-        atomicAdd(&g_stamps[7], n_ci);
-        atomicAdd(&g_stamps[8], n_cs);
+    const int gw = blockIdx.x * (kTraceThreads / 64) + wave;
+    if (lane == 0 && gw < kStampWaves) {  // plain per-wave stores (no contention)
+        unsigned long long* slot = g_stamps + (size_t)gw * 8;
+        for (int k = 0; k < 5; ++k) slot[k] = st[k];
+        slot[5] = 1;
+        slot[6] = n_ct;
+        slot[7] = n_ci | (n_cs << 32);
     }
 #endif
 }
@@ -1236,9 +1238,18 @@ int rt_debug_read_stamps(rt_ctx* ctx, unsigned long long out[16]) {
 #if RT_STAMPS
     HIP_TRY(hipSetDevice(ctx->device));
     HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 16));
-    unsigned long long zero[16] = {};
-    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), zero, sizeof zero));
+    std::vector<unsigned long long> h((size_t)kStampWaves * 8);
+    HIP_TRY(hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(g_stamps), h.size() * 8));
+    for (int k = 0; k < 16; ++k) out[k] = 0;
+    for (size_t w = 0; w < (size_t)kStampWaves; ++w) {
+        const unsigned long long* v = &h[w * 8];
+        for (int k = 0; k < 6; ++k) out[k] += v[k];
+        out[6] += v[6];
+        out[7] += v[7] & 0xffffffffull;
+        out[8] += v[7] >> 32;
+    }
+    std::vector<unsigned long long> z(h.size(), 0);
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z.data(), z.size() * 8));
     return RT_OK;
 #else
     return RT_ERR_UNSUPPORTED;
