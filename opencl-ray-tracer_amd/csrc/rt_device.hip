@@ -86,7 +86,8 @@ struct alignas(16) TriRec {
     double v0x, v0y, p0, p1;
     double inv_det, e1x, e1y, e1z;
     double e2x, e2y, e2z, k0;  // k0 = tz * e1y
-    double k1, dz, pad0, pad1; // k1 = tz * e1x, dz = D
+    double k1, dz;             // k1 = tz * e1x, dz = D
+    float4 colour;             // the cube's colour (carried so shading loads nothing)
 };
 static_assert(sizeof(TriRec) == 128, "TriRec layout");
 
@@ -96,8 +97,9 @@ static_assert(sizeof(TriRec) == 128, "TriRec layout");
 struct alignas(16) SphRec {
     float cx, cy, kzw, tca2;  // kzw = Lz*Lz + Lw*Lw, tca2 = tca*tca
     float r2, tca, pad0, pad1;
+    float4 colour;             // the sphere's colour
 };
-static_assert(sizeof(SphRec) == 32, "SphRec layout");
+static_assert(sizeof(SphRec) == 48, "SphRec layout");
 
 // Per-primitive tile classifier (32 B, fp32, staged in LDS with the box).
 // Triangle: a = (v0x, v0y, au, bu), b = (av, bv, g, 0) with the exact
@@ -176,7 +178,6 @@ __host__ __device__ inline bool prep_triangle(const float* a, const float* b, co
     rec->k0 = tz * e1[1];
     rec->k1 = tz * e1[0];
     rec->dz = dz;
-    rec->pad0 = rec->pad1 = 0.0;
 
     const double eps = 1.1102230246251565e-16;  // 2^-53
     const double mnx = fmin(v0[0], fmin(v1[0], v2[0])), mxx = fmax(v0[0], fmax(v1[0], v2[0]));
@@ -438,19 +439,19 @@ __global__ void __launch_bounds__(kThreads) prep_kernel(
         const float4* v = scene.cube_vertices + 3 * i;
         const float4 a = v[0], bb = v[1], c = v[2];
         const float fa[3] = {a.x, a.y, a.z}, fb[3] = {bb.x, bb.y, bb.z}, fc[3] = {c.x, c.y, c.z};
-        if (i % 12 == 0) colours[i / 12] = scene.cube_colours[i / 12];
         TriRec r{};
         prep_triangle(fa, fb, fc, (double)dir.x, (double)dir.y, (double)dir.z, width, row_begin,
                       row_end, &r, &b, &k, &bad);
+        r.colour = scene.cube_colours[i / 12];
         tri[i] = r;
     } else if (i < n_tri + scene.n_spheres) {
         const int s = i - n_tri;
         const float4 o = scene.sphere_origins[s];
-        colours[scene.n_cubes + s] = scene.sphere_colours[s];
         const float fo[4] = {o.x, o.y, o.z, o.w};
         SphRec r{};
         prep_sphere(fo, scene.sphere_radius[s], dir.x, dir.y, dir.z, dir.w, width, row_begin,
                     row_end, &r, &b, &k, &bad);
+        r.colour = scene.sphere_colours[s];
         sph[s] = r;
     } else {
         return;
@@ -496,11 +497,12 @@ __global__ void __launch_bounds__(kThreads) coarse_kernel(
 // the per-triangle constants (see TriRec); `inside` (wave-uniform) means the
 // tile classifier proved every pixel of the tile passes the u/v tests, so
 // only the exact t is computed.  Spheres: :300-327 on SphRec.
-__device__ __forceinline__ void test_primitive(int p, int slot, bool inside, const Cls& k,
-                                               int n_tri, const TriRec* __restrict__ tri,
+__device__ __forceinline__ void test_primitive(int p, bool inside, const Cls& k, int n_tri,
+                                               const TriRec* __restrict__ tri,
                                                const SphRec* __restrict__ sph, double px,
                                                float pxf, const double* py, const float* pyf,
-                                               float* closest, int* hit) {
+                                               float* closest, float* cr, float* cg,
+                                               float* cb) {
     if (p < n_tri) {
         const TriRec r = tri[p];
         const double tx = px - r.v0x;
@@ -515,7 +517,9 @@ __device__ __forceinline__ void test_primitive(int p, int slot, bool inside, con
                 const float tf = (float)t;
                 if (tf < closest[j]) {
                     closest[j] = tf;
-                    hit[j] = slot;
+                    cr[j] = r.colour.x;
+                    cg[j] = r.colour.y;
+                    cb[j] = r.colour.z;
                 }
             }
             return;
@@ -559,7 +563,9 @@ __device__ __forceinline__ void test_primitive(int p, int slot, bool inside, con
                 const float tf = (float)t;
                 if (tf < closest[j]) {
                     closest[j] = tf;
-                    hit[j] = slot;
+                    cr[j] = r.colour.x;
+                    cg[j] = r.colour.y;
+                    cb[j] = r.colour.z;
                 }
             }
         }
@@ -577,7 +583,9 @@ __device__ __forceinline__ void test_primitive(int p, int slot, bool inside, con
                 const float t0 = s.tca - thc;
                 if (t0 != 0.0f && t0 < closest[j]) {
                     closest[j] = t0;
-                    hit[j] = slot;
+                    cr[j] = s.colour.x;
+                    cg[j] = s.colour.y;
+                    cb[j] = s.colour.z;
                 }
             }
         }
@@ -649,8 +657,15 @@ __device__ unsigned long long g_stamps[kStampWaves * 8];
 // and filter candidates but skip the per-pixel tests, 3 = everything but the
 // framebuffer stores, 4 = per-pixel tests without the per-candidate record
 // loads (wrong pixels; timing only).
+#ifndef RT_WPE
+#define RT_WPE 0                  // >0: ask the allocator for this many waves per SIMD
+#endif
 template <int kMode>
-__global__ void __launch_bounds__(kTraceThreads) trace_kernel(
+__global__ void __launch_bounds__(kTraceThreads)
+#if RT_WPE > 0
+__attribute__((amdgpu_waves_per_eu(RT_WPE)))
+#endif
+trace_kernel(
     SceneDev scene, const TriRec* __restrict__ tri, const SphRec* __restrict__ sph,
     const int4* __restrict__ boxes, const Cls* __restrict__ cls,
     const float4* __restrict__ colours, const int* __restrict__ counts,
@@ -686,14 +701,14 @@ __global__ void __launch_bounds__(kTraceThreads) trace_kernel(
         return;
     }
 
-    float closest[kRowsPerLane];
-    int hit[kRowsPerLane];  // colour slot of the closest primitive, -1 = none
+    float closest[kRowsPerLane];  // kFar = no hit (a hit always sets closest < kFar)
+    float cr[kRowsPerLane], cg[kRowsPerLane], cb[kRowsPerLane];  // its colour
     double py[kRowsPerLane];
     float pyf[kRowsPerLane];
 #pragma unroll
     for (int j = 0; j < kRowsPerLane; ++j) {
         closest[j] = kFar;
-        hit[j] = -1;
+        cr[j] = cg[j] = cb[j] = 0.0f;
         py[j] = (double)(y0 + kLaneRows * j);
         pyf[j] = (float)(y0 + kLaneRows * j);
     }
@@ -705,9 +720,9 @@ __global__ void __launch_bounds__(kTraceThreads) trace_kernel(
     unsigned long long n_ct = 0, n_ci = 0, n_cs = 0;
     (void)st; (void)ta; (void)tb; (void)n_ct; (void)n_ci; (void)n_cs;
     STAMP(ta);
-    const int cb = (bin_y / kCoarse) * n_cx + bin_x / kCoarse;
-    const int count = kMode == 1 ? 0 : counts[cb];
-    const int* __restrict__ list = lists + (int64_t)cb * cap;
+    const int coarse = (bin_y / kCoarse) * n_cx + bin_x / kCoarse;
+    const int count = kMode == 1 ? 0 : counts[coarse];
+    const int* __restrict__ list = lists + (int64_t)coarse * cap;
     int* wlist = s_wlist[wave];
     for (int s0 = 0; s0 < count; s0 += kStage) {
         const int n = min(kStage, count - s0);
@@ -761,7 +776,7 @@ __global__ void __launch_bounds__(kTraceThreads) trace_kernel(
             const int v = __builtin_amdgcn_readfirstlane(wlist[i]);
             const int p = v & 0x7fffffff;
             if (kMode == 2) {
-                hit[0] = hit[0] > p ? hit[0] : -1;  // keep the walk alive
+                cr[0] = cr[0] > (float)p ? cr[0] : 0.0f;  // keep the walk alive
                 continue;
             }
 #if RT_STAMPS
@@ -769,11 +784,10 @@ __global__ void __launch_bounds__(kTraceThreads) trace_kernel(
             n_ci += p < n_tri && v < 0;
             n_cs += p >= n_tri;
 #endif
-            const int slot = p < n_tri ? p / 12 : scene.n_cubes + (p - n_tri);
             // kMode 4: same tests on record 0 / sphere 0 (no dependent record loads)
             const int pr = kMode == 4 ? (p < n_tri ? 0 : n_tri) : p;
-            test_primitive(pr, slot, v < 0, Cls{}, n_tri, tri, sph, px, pxf, py, pyf, closest,
-                           hit);
+            test_primitive(pr, v < 0, Cls{}, n_tri, tri, sph, px, pxf, py, pyf, closest, cr, cg,
+                           cb);
         }
         STAMP(tb);
 #if RT_STAMPS
@@ -782,17 +796,14 @@ __global__ void __launch_bounds__(kTraceThreads) trace_kernel(
 #endif
     }
 
-    // Shade + store.  A wave whose pixels all missed (ballot) stores the
-    // black pattern without touching the colour table.
-    bool lane_hit = false;
-#pragma unroll
-    for (int j = 0; j < kRowsPerLane; ++j) lane_hit |= hit[j] >= 0;
-    const bool any_hit = __ballot(lane_hit) != 0ull;
+    // Shade + store.  The winning colour travelled with closest (scalar-loaded
+    // with each candidate's record), so shading touches no memory.
     int4v pix[kRowsPerLane];
 #pragma unroll
     for (int j = 0; j < kRowsPerLane; ++j) {
         pix[j] = int4v{0, 0, 0, 255};
-        if (any_hit && hit[j] >= 0) pix[j] = shade_hit(closest[j], colours[hit[j]]);
+        if (closest[j] != kFar)
+            pix[j] = shade_hit(closest[j], make_float4(cr[j], cg[j], cb[j], 0.0f));
     }
 #if RT_STAMPS
     asm volatile("" ::"v"(pix[0].x), "v"(pix[kRowsPerLane - 1].z));
