@@ -428,8 +428,7 @@ __global__ void __launch_bounds__(kThreads) generic_kernel(
 __global__ void __launch_bounds__(kThreads) prep_kernel(
     SceneDev scene, float4 dir, int width, int row_begin, int row_end,
     TriRec* __restrict__ tri, SphRec* __restrict__ sph, int4* __restrict__ boxes,
-    Cls* __restrict__ cls, float4* __restrict__ colours, unsigned* __restrict__ nonfinite_flag,
-    unsigned gen) {
+    Cls* __restrict__ cls, unsigned* __restrict__ nonfinite_flag, unsigned gen) {
     const int n_tri = 12 * scene.n_cubes;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     Box b = empty_box();
@@ -646,17 +645,24 @@ __device__ unsigned long long g_stamps[kStampWaves * 8];
 #define STAMP(t) do { } while (0)
 #endif
 
-// One workgroup per bin (2x2 wave tiles), kRowsPerLane pixels per lane.
-// The parent coarse bin's candidate list (ids, boxes, classifiers) is staged
-// in LDS once per workgroup; each wave filters it against its own tile (one
-// ballot per 64 entries, compacted in order into a per-wave LDS list with the
-// tile classification in bit 31), then walks that list with one flat uniform
-// loop: scalar record loads -> per-lane exact tests.
+// One workgroup per 64x64 coarse bin (4 waves); each wave renders
+// kTilesPerWave tiles of kWaveTile x kWaveTileH pixels, kRowsPerLane pixels
+// per lane.  The coarse bin's candidate list (ids, boxes, classifiers) is
+// staged in LDS once per workgroup; for each tile the wave filters it (one
+// ballot per 64 entries, compacted in order into a per-wave LDS list with
+// the tile classification in bit 31), walks that list with one flat uniform
+// loop (scalar record loads -> per-lane exact tests; the winning colour
+// travels with `closest`), then shades and stores -- and moves on to the
+// next tile while those stores drain.
 // kMode is a diagnostics ablation (rt_debug_set_trace_mode): 0 = the real
 // kernel, 1 = stores only (the store floor of this exact pattern), 2 = stage
 // and filter candidates but skip the per-pixel tests, 3 = everything but the
-// framebuffer stores, 4 = per-pixel tests without the per-candidate record
-// loads (wrong pixels; timing only).
+// framebuffer stores, 4 = per-pixel tests against records 0 / n_tri only
+// (wrong pixels; timing only).
+constexpr int kTilesX = kCoarse / kWaveTile, kTilesY = kCoarse / kWaveTileH;
+constexpr int kTilesPerWave = kTilesX * kTilesY / (kTraceThreads / 64);
+static_assert(kTilesPerWave * (kTraceThreads / 64) == kTilesX * kTilesY, "tiles per wave");
+
 #ifndef RT_WPE
 #define RT_WPE 0                  // >0: ask the allocator for this many waves per SIMD
 #endif
@@ -667,163 +673,190 @@ __attribute__((amdgpu_waves_per_eu(RT_WPE)))
 #endif
 trace_kernel(
     SceneDev scene, const TriRec* __restrict__ tri, const SphRec* __restrict__ sph,
-    const int4* __restrict__ boxes, const Cls* __restrict__ cls,
-    const float4* __restrict__ colours, const int* __restrict__ counts,
+    const int4* __restrict__ boxes, const Cls* __restrict__ cls, const int* __restrict__ counts,
     const int* __restrict__ lists, int cap, const unsigned* __restrict__ nonfinite_flag,
-    unsigned gen, float4 dir, int width, int row_begin, int row_end, int n_bins_x, int n_cx,
-    int out_format, void* __restrict__ out) {
+    unsigned gen, float4 dir, int width, int row_begin, int row_end, int n_cx, int out_format,
+    void* __restrict__ out) {
     __shared__ int s_id[kStage];
     __shared__ int4 s_box[kStage];
     __shared__ Cls s_cls[kStage];
     __shared__ int s_wlist[kTraceThreads / 64][kStage];
-    const int bin = blockIdx.x;
+    const int coarse = blockIdx.x;
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
-    const int bin_x = (bin % n_bins_x) * kBinW;
-    const int bin_y = (bin / n_bins_x) * kBinH;  // relative to row_begin
-    const int tile_x = bin_x + (wave % kWavesX) * kWaveTile;
-    const int tile_y = row_begin + bin_y + (wave / kWavesX) * kWaveTileH;
-    const int x = tile_x + (lane % kWaveTile);
-    const int y0 = tile_y + (lane / kWaveTile);
+    const int block_x = (coarse % n_cx) * kCoarse;
+    const int block_y = row_begin + (coarse / n_cx) * kCoarse;
     const int n_tri = 12 * scene.n_cubes;
+    const int lx = lane % kWaveTile, ly = lane / kWaveTile;
 
     if (kMode == 0 && *nonfinite_flag == gen) {
         // Non-finite scene data: the algebraic shortcuts of the binned path
         // assume finite values, so run the reference algorithm verbatim.
 #pragma unroll 1
-        for (int j = 0; j < kRowsPerLane; ++j) {
-            const int y = y0 + kLaneRows * j;
-            if (x >= width || y >= row_end) continue;
-            const int4v p =
-                collide_generic(scene, make_float4((float)x, (float)y, 0.0f, 1.0f), dir);
-            store_pixel(out, out_format, (int64_t)(y - row_begin) * width + x, p);
+        for (int k = 0; k < kTilesPerWave; ++k) {
+            const int t = wave + (kTraceThreads / 64) * k;
+            const int x = block_x + (t % kTilesX) * kWaveTile + lx;
+#pragma unroll 1
+            for (int j = 0; j < kRowsPerLane; ++j) {
+                const int y = block_y + (t / kTilesX) * kWaveTileH + ly + kLaneRows * j;
+                if (x >= width || y >= row_end) continue;
+                const int4v p =
+                    collide_generic(scene, make_float4((float)x, (float)y, 0.0f, 1.0f), dir);
+                store_pixel(out, out_format, (int64_t)(y - row_begin) * width + x, p);
+            }
         }
         return;
     }
-
-    float closest[kRowsPerLane];  // kFar = no hit (a hit always sets closest < kFar)
-    float cr[kRowsPerLane], cg[kRowsPerLane], cb[kRowsPerLane];  // its colour
-    double py[kRowsPerLane];
-    float pyf[kRowsPerLane];
-#pragma unroll
-    for (int j = 0; j < kRowsPerLane; ++j) {
-        closest[j] = kFar;
-        cr[j] = cg[j] = cb[j] = 0.0f;
-        py[j] = (double)(y0 + kLaneRows * j);
-        pyf[j] = (float)(y0 + kLaneRows * j);
-    }
-    const double px = (double)x;
-    const float pxf = (float)x;
-    const int tx1 = tile_x + kWaveTile - 1, ty1 = tile_y + kWaveTileH - 1;
 
     unsigned long long st[6] = {0, 0, 0, 0, 0, 0}, ta = 0, tb = 0;
     unsigned long long n_ct = 0, n_ci = 0, n_cs = 0;
     (void)st; (void)ta; (void)tb; (void)n_ct; (void)n_ci; (void)n_cs;
     STAMP(ta);
-    const int coarse = (bin_y / kCoarse) * n_cx + bin_x / kCoarse;
     const int count = kMode == 1 ? 0 : counts[coarse];
     const int* __restrict__ list = lists + (int64_t)coarse * cap;
     int* wlist = s_wlist[wave];
-    for (int s0 = 0; s0 < count; s0 += kStage) {
-        const int n = min(kStage, count - s0);
-        if (s0 > 0) __syncthreads();  // previous stage fully consumed
+    const bool one_stage = count <= kStage;
+
+    auto stage = [&](int s0, int n) {
         for (int i = threadIdx.x; i < n; i += kTraceThreads) {
             const int id = list[s0 + i];
             s_id[i] = id;
             s_box[i] = boxes[id];
             s_cls[i] = cls[id];
         }
+    };
+    if (one_stage && count > 0) {
+        stage(0, count);
         __syncthreads();
-        STAMP(tb);
-#if RT_STAMPS
-        st[0] += tb - ta;
-        ta = tb;
-#endif
-        // filter: this wave's candidates, in order, into wlist
-        int wn = 0;
-        for (int c = 0; c < n; c += 64) {
-            const int e = c + lane;
-            bool keep = false, inside = false;
-            int id = 0;
-            if (e < n) {
-                const int4 b = s_box[e];
-                id = s_id[e];
-                if (b.x <= tx1 && b.z >= tile_x && b.y <= ty1 && b.w >= tile_y) {
-#if RT_TILECLS
-                    classify(s_cls[e], id < n_tri, (float)tile_x, (float)tile_y, &keep, &inside);
-#else
-                    keep = true;
-#endif
-                }
-            }
-            const unsigned long long m = __ballot(keep);
-            if (keep) {
-                const unsigned below = __builtin_amdgcn_mbcnt_hi(
-                    (unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-                wlist[wn + (int)below] = id | (inside ? (int)0x80000000u : 0);
-            }
-            wn += __popcll(m);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        STAMP(tb);
-#if RT_STAMPS
-        st[1] += tb - ta;
-        ta = tb;
-#endif
-        for (int i = 0; i < wn; ++i) {
-            const int v = __builtin_amdgcn_readfirstlane(wlist[i]);
-            const int p = v & 0x7fffffff;
-            if (kMode == 2) {
-                cr[0] = cr[0] > (float)p ? cr[0] : 0.0f;  // keep the walk alive
-                continue;
-            }
-#if RT_STAMPS
-            n_ct += p < n_tri;
-            n_ci += p < n_tri && v < 0;
-            n_cs += p >= n_tri;
-#endif
-            // kMode 4: same tests on record 0 / sphere 0 (no dependent record loads)
-            const int pr = kMode == 4 ? (p < n_tri ? 0 : n_tri) : p;
-            test_primitive(pr, v < 0, Cls{}, n_tri, tri, sph, px, pxf, py, pyf, closest, cr, cg,
-                           cb);
-        }
-        STAMP(tb);
-#if RT_STAMPS
-        st[2] += tb - ta;
-        ta = tb;
-#endif
     }
-
-    // Shade + store.  The winning colour travelled with closest (scalar-loaded
-    // with each candidate's record), so shading touches no memory.
-    int4v pix[kRowsPerLane];
-#pragma unroll
-    for (int j = 0; j < kRowsPerLane; ++j) {
-        pix[j] = int4v{0, 0, 0, 255};
-        if (closest[j] != kFar)
-            pix[j] = shade_hit(closest[j], make_float4(cr[j], cg[j], cb[j], 0.0f));
-    }
-#if RT_STAMPS
-    asm volatile("" ::"v"(pix[0].x), "v"(pix[kRowsPerLane - 1].z));
-#endif
     STAMP(tb);
 #if RT_STAMPS
-    st[3] += tb - ta;
+    st[0] += tb - ta;
     ta = tb;
 #endif
+
+#pragma unroll 1
+    for (int k = 0; k < kTilesPerWave; ++k) {
+        const int t = wave + (kTraceThreads / 64) * k;
+        const int tile_x = block_x + (t % kTilesX) * kWaveTile;
+        const int tile_y = block_y + (t / kTilesX) * kWaveTileH;
+        // tiles wholly outside the frame / band (uniform; no barriers follow
+        // on the one-stage path, so skipping is safe there)
+        if (one_stage && (tile_x >= width || tile_y >= row_end)) continue;
+        const int x = tile_x + lx;
+        const int y0 = tile_y + ly;
+        const int tx1 = tile_x + kWaveTile - 1, ty1 = tile_y + kWaveTileH - 1;
+
+        float closest[kRowsPerLane];  // kFar = no hit (a hit always sets closest < kFar)
+        float cr[kRowsPerLane], cg[kRowsPerLane], cb[kRowsPerLane];  // its colour
+        double py[kRowsPerLane];
+        float pyf[kRowsPerLane];
 #pragma unroll
-    for (int j = 0; j < kRowsPerLane; ++j) {
-        const int y = y0 + kLaneRows * j;
-        // kMode 3: everything but the stores (a store the compiler cannot drop)
-        const bool store = kMode != 3 || pix[j].x == 0x7fffffff;
-        if (x < width && y < row_end && store)
-            store_pixel(out, out_format, (int64_t)(y - row_begin) * width + x, pix[j]);
-    }
-    STAMP(tb);
+        for (int j = 0; j < kRowsPerLane; ++j) {
+            closest[j] = kFar;
+            cr[j] = cg[j] = cb[j] = 0.0f;
+            py[j] = (double)(y0 + kLaneRows * j);
+            pyf[j] = (float)(y0 + kLaneRows * j);
+        }
+        const double px = (double)x;
+        const float pxf = (float)x;
+
+        for (int s0 = 0; s0 < count; s0 += kStage) {
+            const int n = min(kStage, count - s0);
+            if (!one_stage) {  // uniform across the workgroup
+                __syncthreads();
+                stage(s0, n);
+                __syncthreads();
+            }
+            // filter: this wave's candidates for this tile, in order
+            int wn = 0;
+            for (int c = 0; c < n; c += 64) {
+                const int e = c + lane;
+                bool keep = false, inside = false;
+                int id = 0;
+                if (e < n) {
+                    const int4 b = s_box[e];
+                    id = s_id[e];
+                    if (b.x <= tx1 && b.z >= tile_x && b.y <= ty1 && b.w >= tile_y) {
+#if RT_TILECLS
+                        classify(s_cls[e], id < n_tri, (float)tile_x, (float)tile_y, &keep,
+                                 &inside);
+#else
+                        keep = true;
+#endif
+                    }
+                }
+                const unsigned long long m = __ballot(keep);
+                if (keep) {
+                    const unsigned below = __builtin_amdgcn_mbcnt_hi(
+                        (unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+                    wlist[wn + (int)below] = id | (inside ? (int)0x80000000u : 0);
+                }
+                wn += __popcll(m);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            STAMP(tb);
 #if RT_STAMPS
-    st[4] += tb - ta;
+            st[1] += tb - ta;
+            ta = tb;
+#endif
+            for (int i = 0; i < wn; ++i) {
+                const int v = __builtin_amdgcn_readfirstlane(wlist[i]);
+                const int p = v & 0x7fffffff;
+                if (kMode == 2) {
+                    cr[0] = cr[0] > (float)p ? cr[0] : 0.0f;  // keep the walk alive
+                    continue;
+                }
+#if RT_STAMPS
+                n_ct += p < n_tri;
+                n_ci += p < n_tri && v < 0;
+                n_cs += p >= n_tri;
+#endif
+                const int pr = kMode == 4 ? (p < n_tri ? 0 : n_tri) : p;
+                test_primitive(pr, v < 0, Cls{}, n_tri, tri, sph, px, pxf, py, pyf, closest, cr,
+                               cg, cb);
+            }
+            STAMP(tb);
+#if RT_STAMPS
+            st[2] += tb - ta;
+            ta = tb;
+#endif
+        }
+
+        // Shade + store.  The winning colour travelled with closest (scalar-
+        // loaded with each candidate's record), so shading touches no memory.
+        int4v pix[kRowsPerLane];
+#pragma unroll
+        for (int j = 0; j < kRowsPerLane; ++j) {
+            pix[j] = int4v{0, 0, 0, 255};
+            if (closest[j] != kFar)
+                pix[j] = shade_hit(closest[j], make_float4(cr[j], cg[j], cb[j], 0.0f));
+        }
+#if RT_STAMPS
+        asm volatile("" ::"v"(pix[0].x), "v"(pix[kRowsPerLane - 1].z));
+#endif
+        STAMP(tb);
+#if RT_STAMPS
+        st[3] += tb - ta;
+        ta = tb;
+#endif
+#pragma unroll
+        for (int j = 0; j < kRowsPerLane; ++j) {
+            const int y = y0 + kLaneRows * j;
+            // kMode 3: everything but the stores (a store the compiler cannot drop)
+            const bool store = kMode != 3 || pix[j].x == 0x7fffffff;
+            if (x < width && y < row_end && store)
+                store_pixel(out, out_format, (int64_t)(y - row_begin) * width + x, pix[j]);
+        }
+        STAMP(tb);
+#if RT_STAMPS
+        st[4] += tb - ta;
+        ta = tb;
+#endif
+    }
+#if RT_STAMPS
     const int gw = blockIdx.x * (kTraceThreads / 64) + wave;
     if (lane == 0 && gw < kStampWaves) {  // plain per-wave stores (no contention)
         unsigned long long* slot = g_stamps + (size_t)gw * 8;
@@ -954,14 +987,10 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
     }
     const int n_tri = 12 * s->num_cubes;
     const int n_prims = n_tri + s->num_spheres;
-    const int n_bins_x = (width + kBinW - 1) / kBinW;
-    const int n_bins_y = (rows + kBinH - 1) / kBinH;
     const int n_cx = (width + kCoarse - 1) / kCoarse;
     const int n_cy = (rows + kCoarse - 1) / kCoarse;
-    const int64_t n_bins64 = (int64_t)n_bins_x * n_bins_y;
     const int64_t n_coarse64 = (int64_t)n_cx * n_cy;
-    if (n_bins64 >= (int64_t)1 << 31) return RT_ERR_INVALID_ARG;
-    const int n_bins = (int)n_bins64;
+    if (n_coarse64 >= (int64_t)1 << 31) return RT_ERR_INVALID_ARG;
     const int n_coarse = (int)n_coarse64;
     const int cap = n_prims > 0 ? n_prims : 1;
 
@@ -969,9 +998,7 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
     const size_t sph_off = align_up(sizeof(TriRec) * (size_t)n_tri, 256);
     const size_t box_off = sph_off + align_up(sizeof(SphRec) * (size_t)s->num_spheres, 256);
     const size_t cls_off = box_off + align_up(sizeof(int4) * (size_t)n_prims, 256);
-    const size_t col_off = cls_off + align_up(sizeof(Cls) * (size_t)n_prims, 256);
-    const size_t cnt_off =
-        col_off + align_up(sizeof(float4) * (size_t)(s->num_cubes + s->num_spheres), 256);
+    const size_t cnt_off = cls_off + align_up(sizeof(Cls) * (size_t)n_prims, 256);
     const size_t rec_need = cnt_off + align_up(sizeof(int) * (size_t)n_coarse, 256);
     int rc = ensure(&ctx->rec_buf, &ctx->rec_cap, rec_need);
     if (rc) return rc;
@@ -983,7 +1010,6 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
     SphRec* sph = reinterpret_cast<SphRec*>(base + sph_off);
     int4* boxes = reinterpret_cast<int4*>(base + box_off);
     Cls* clsv = reinterpret_cast<Cls*>(base + cls_off);
-    float4* colours = reinterpret_cast<float4*>(base + col_off);
     int* counts = reinterpret_cast<int*>(base + cnt_off);
     int* lists = static_cast<int*>(ctx->list_buf);
     // generation-stamped non-finite flag: no per-launch memset needed
@@ -994,8 +1020,7 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
 
     if (n_prims > 0) {
         prep_kernel<<<dim3((n_prims + kThreads - 1) / kThreads), dim3(kThreads), 0, stream>>>(
-            sd, dir, width, row_begin, row_end, tri, sph, boxes, clsv, colours, ctx->flag,
-            ctx->gen);
+            sd, dir, width, row_begin, row_end, tri, sph, boxes, clsv, ctx->flag, ctx->gen);
         HIP_TRY(hipGetLastError());
     }
     if (pe) HIP_TRY(hipEventRecord(pe[1], stream));
@@ -1007,10 +1032,9 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
               : ctx->trace_mode == 2 ? trace_kernel<2>
               : ctx->trace_mode == 3 ? trace_kernel<3>
               : ctx->trace_mode == 4 ? trace_kernel<4> : trace_kernel<0>;
-    kern<<<dim3((unsigned)n_bins), dim3(kTraceThreads), 0, stream>>>(
-        sd, tri, sph, boxes, clsv, colours, counts, lists, cap, ctx->flag, ctx->gen, dir, width,
-        row_begin,
-        row_end, n_bins_x, n_cx, fmt, out);
+    kern<<<dim3((unsigned)n_coarse), dim3(kTraceThreads), 0, stream>>>(
+        sd, tri, sph, boxes, clsv, counts, lists, cap, ctx->flag, ctx->gen, dir, width, row_begin,
+        row_end, n_cx, fmt, out);
     HIP_TRY(hipGetLastError());
     if (pe) HIP_TRY(hipEventRecord(pe[3], stream));
     return RT_OK;
