@@ -794,9 +794,11 @@ trace_kernel(
                 }
                 wn += __popcll(m);
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // wlist was written by other lanes of this wave: LDS ops of one
+            // wave complete in order, so waiting on lgkmcnt (not a release
+            // fence, which would also wait for the previous tile's stores)
+            // and a compiler barrier suffice.
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             STAMP(tb);
 #if RT_STAMPS
             st[1] += tb - ta;
