@@ -51,6 +51,9 @@ namespace {
 #ifndef RT_STAMPS
 #define RT_STAMPS 0               // diagnostics build: per-phase s_memtime sums
 #endif
+#ifndef RT_LDSREC
+#define RT_LDSREC 0               // stage candidate records in LDS (per workgroup)
+#endif
 #ifndef RT_PIXCLS
 #define RT_PIXCLS 0               // per-pixel fp32 pre-classification
 #endif
@@ -591,6 +594,99 @@ __device__ __forceinline__ void test_primitive(int p, bool inside, const Cls& k,
     }
 }
 
+__device__ __forceinline__ void test_record(bool is_tri, bool inside, const Cls& k,
+                                            const TriRec& r, double px, float pxf,
+                                            const double* py, const float* pyf, float* closest,
+                                            float* cr, float* cg, float* cb) {
+    if (is_tri) {
+        const double tx = px - r.v0x;
+        if (inside) {
+#pragma unroll
+            for (int j = 0; j < kRowsPerLane; ++j) {
+                const double ty = py[j] - r.v0y;
+                const double q2 = tx * r.e1y - ty * r.e1x;
+                const double q0 = ty * r.e1z - r.k0;
+                const double q1 = r.k1 - tx * r.e1z;
+                const double t = (r.e2x * q0 + r.e2y * q1 + r.e2z * q2) * r.inv_det;
+                const float tf = (float)t;
+                if (tf < closest[j]) {
+                    closest[j] = tf;
+                    cr[j] = r.colour.x;
+                    cg[j] = r.colour.y;
+                    cb[j] = r.colour.z;
+                }
+            }
+            return;
+        }
+        // Partial tile: classify each pixel on the fp32 planes first (same
+        // margin as the tile classifier); only pixels inside the margin band
+        // of an edge run the full fp64 u/v test, proven-inside pixels compute
+        // t only, proven-outside pixels are done.
+#if RT_PIXCLS
+        const float xl = pxf - k.a.x;
+        const float ux = k.a.z * xl, vx = k.b.x * xl;
+        const float g = k.b.z;
+#endif
+#pragma unroll
+        for (int j = 0; j < kRowsPerLane; ++j) {
+#if RT_PIXCLS
+            const float yl = pyf[j] - k.a.y;
+            const float ul = ux + k.a.w * yl;
+            const float vl = vx + k.b.y * yl;
+            const float wl = ul + vl;
+            const bool out = ul < -g || ul > 1.0f + g || vl < -g || vl > 1.0f + g || wl > 1.0f + g;
+            const bool in = ul > g && ul < 1.0f - g && vl > g && vl < 1.0f - g && wl < 1.0f - g;
+            if (out) continue;
+#else
+            const bool in = false;
+#endif
+            const double ty = py[j] - r.v0y;
+            const double q2 = tx * r.e1y - ty * r.e1x;
+            bool pass = in;
+            if (!in) {
+                // u = ((tx*p0 + ty*p1) + tz*p2) * inv_det, tz*p2 == +-0 for d = (0,0,D)
+                const double u = (tx * r.p0 + ty * r.p1) * r.inv_det;
+                // v = ((d0*q0 + d1*q1) + d2*q2) * inv_det, d0 = d1 = +-0
+                const double v = (r.dz * q2) * r.inv_det;
+                pass = !(u < 0.0 || u > 1.0) && !(v < 0.0 || u + v > 1.0);
+            }
+            if (pass) {
+                const double q0 = ty * r.e1z - r.k0;
+                const double q1 = r.k1 - tx * r.e1z;
+                const double t = (r.e2x * q0 + r.e2y * q1 + r.e2z * q2) * r.inv_det;
+                const float tf = (float)t;
+                if (tf < closest[j]) {
+                    closest[j] = tf;
+                    cr[j] = r.colour.x;
+                    cg[j] = r.colour.y;
+                    cb[j] = r.colour.z;
+                }
+            }
+        }
+    } else {
+        SphRec s;
+        __builtin_memcpy(&s, &r, sizeof s);  // spheres share the 128-B slots
+        const float lx = s.cx - pxf;
+        const float lx2 = lx * lx;
+#pragma unroll
+        for (int j = 0; j < kRowsPerLane; ++j) {
+            const float ly = s.cy - pyf[j];
+            const float a = lx2 + ly * ly;
+            const float dist2 = (a + s.kzw) - s.tca2;
+            if (!(dist2 > s.r2)) {
+                const float thc = sqrtf(s.r2 - dist2);
+                const float t0 = s.tca - thc;
+                if (t0 != 0.0f && t0 < closest[j]) {
+                    closest[j] = t0;
+                    cr[j] = s.colour.x;
+                    cg[j] = s.colour.y;
+                    cb[j] = s.colour.z;
+                }
+            }
+        }
+    }
+}
+
 [[maybe_unused]] __device__ __forceinline__ float readlane_f(float v, int lane) {
     return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), lane));
 }
@@ -681,6 +777,9 @@ trace_kernel(
     __shared__ int4 s_box[kStage];
     __shared__ Cls s_cls[kStage];
     __shared__ int s_wlist[kTraceThreads / 64][kStage];
+#if RT_LDSREC
+    __shared__ TriRec s_rec[kStage];
+#endif
     const int coarse = blockIdx.x;
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
@@ -724,6 +823,19 @@ trace_kernel(
             s_box[i] = boxes[id];
             s_cls[i] = cls[id];
         }
+#if RT_LDSREC
+        // candidate records, 16 B per lane (spheres: the 48-B SphRec)
+        for (int i = threadIdx.x; i < n * 8; i += kTraceThreads) {
+            const int id = list[s0 + (i >> 3)];
+            const int part = i & 7;
+            float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            if (id < n_tri)
+                v = reinterpret_cast<const float4*>(tri + id)[part];
+            else if (part < 3)
+                v = reinterpret_cast<const float4*>(sph + (id - n_tri))[part];
+            reinterpret_cast<float4*>(s_rec)[i] = v;
+        }
+#endif
     };
     if (one_stage && count > 0) {
         stage(0, count);
@@ -790,7 +902,12 @@ trace_kernel(
                 if (keep) {
                     const unsigned below = __builtin_amdgcn_mbcnt_hi(
                         (unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+#if RT_LDSREC
+                    wlist[wn + (int)below] = e | (id < n_tri ? 0x40000000 : 0) |
+                                             (inside ? (int)0x80000000u : 0);
+#else
                     wlist[wn + (int)below] = id | (inside ? (int)0x80000000u : 0);
+#endif
                 }
                 wn += __popcll(m);
             }
@@ -804,7 +921,18 @@ trace_kernel(
             st[1] += tb - ta;
             ta = tb;
 #endif
+#if RT_LDSREC
+            for (int i = 0; i < wn && kMode != 2; ++i) {
+                const int v = __builtin_amdgcn_readfirstlane(wlist[i]);
+                const int e = v & 0x3fffffff;
+                const TriRec r = s_rec[kMode == 4 ? 0 : e];
+                test_record((v & 0x40000000) != 0, v < 0, Cls{}, r, px, pxf, py, pyf, closest,
+                            cr, cg, cb);
+            }
+            for (int i = 0; i < wn && kMode == 2; ++i) {
+#else
             for (int i = 0; i < wn; ++i) {
+#endif
                 const int v = __builtin_amdgcn_readfirstlane(wlist[i]);
                 const int p = v & 0x7fffffff;
                 if (kMode == 2) {
@@ -816,9 +944,11 @@ trace_kernel(
                 n_ci += p < n_tri && v < 0;
                 n_cs += p >= n_tri;
 #endif
+#if !RT_LDSREC
                 const int pr = kMode == 4 ? (p < n_tri ? 0 : n_tri) : p;
                 test_primitive(pr, v < 0, Cls{}, n_tri, tri, sph, px, pxf, py, pyf, closest, cr,
                                cg, cb);
+#endif
             }
             STAMP(tb);
 #if RT_STAMPS
