@@ -40,19 +40,13 @@ namespace {
 
 // Build-time geometry / feature knobs (A/B variants: scripts/variants.sh).
 #ifndef RT_TILE_W
-#define RT_TILE_W 16              // wave tile width (lanes per row)
+#define RT_TILE_W 8               // wave tile width (lanes per row)
 #endif
 #ifndef RT_ROWS
 #define RT_ROWS 4                 // pixels per lane (rows, 64/RT_TILE_W apart)
 #endif
 #ifndef RT_TILECLS
 #define RT_TILECLS 1              // per-tile plane classification of candidates
-#endif
-#ifndef RT_STAMPS
-#define RT_STAMPS 0               // diagnostics build: per-phase s_memtime sums
-#endif
-#ifndef RT_LDSREC
-#define RT_LDSREC 0               // stage candidate records in LDS (per workgroup)
 #endif
 #ifndef RT_PIXCLS
 #define RT_PIXCLS 0               // per-pixel fp32 pre-classification
@@ -61,20 +55,13 @@ constexpr int kWaveTile = RT_TILE_W;                       // wave tile width
 constexpr int kRowsPerLane = RT_ROWS;
 constexpr int kLaneRows = 64 / RT_TILE_W;                  // lane rows per pass
 constexpr int kWaveTileH = kLaneRows * RT_ROWS;            // wave tile height
-#ifndef RT_WAVES_X
-#define RT_WAVES_X 2              // wave tiles per trace workgroup, x
-#endif
-#ifndef RT_WAVES_Y
-#define RT_WAVES_Y 2              // wave tiles per trace workgroup, y
-#endif
-constexpr int kWavesX = RT_WAVES_X, kWavesY = RT_WAVES_Y;
-constexpr int kTraceThreads = 64 * kWavesX * kWavesY;
-constexpr int kBinW = kWavesX * kWaveTile;  // bin = trace workgroup tile
-constexpr int kBinH = kWavesY * kWaveTileH;
+constexpr int kBinW = 2 * kWaveTile;  // bin = workgroup tile (2x2 wave tiles)
+constexpr int kBinH = 2 * kWaveTileH;
 constexpr int kCoarse = 64;       // coarse bin (candidate list) edge, pixels
 constexpr int kStage = 256;       // candidate entries staged in LDS per pass
 static_assert(64 % kBinW == 0 && 64 % kBinH == 0, "bins must tile a coarse bin");
 constexpr int kThreads = 256;
+constexpr int kPrepThreads = 64;  // prep: one wave per block, spread over CUs
 constexpr double kEpsilon = 0.000001;      // MainState.cpp:15
 constexpr float kFar = 300000.0f;          // MainState.cpp:345
 
@@ -89,8 +76,7 @@ struct alignas(16) TriRec {
     double v0x, v0y, p0, p1;
     double inv_det, e1x, e1y, e1z;
     double e2x, e2y, e2z, k0;  // k0 = tz * e1y
-    double k1, dz;             // k1 = tz * e1x, dz = D
-    float4 colour;             // the cube's colour (carried so shading loads nothing)
+    double k1, dz, pad0, pad1; // k1 = tz * e1x, dz = D
 };
 static_assert(sizeof(TriRec) == 128, "TriRec layout");
 
@@ -100,9 +86,8 @@ static_assert(sizeof(TriRec) == 128, "TriRec layout");
 struct alignas(16) SphRec {
     float cx, cy, kzw, tca2;  // kzw = Lz*Lz + Lw*Lw, tca2 = tca*tca
     float r2, tca, pad0, pad1;
-    float4 colour;             // the sphere's colour
 };
-static_assert(sizeof(SphRec) == 48, "SphRec layout");
+static_assert(sizeof(SphRec) == 32, "SphRec layout");
 
 // Per-primitive tile classifier (32 B, fp32, staged in LDS with the box).
 // Triangle: a = (v0x, v0y, au, bu), b = (av, bv, g, 0) with the exact
@@ -181,6 +166,7 @@ __host__ __device__ inline bool prep_triangle(const float* a, const float* b, co
     rec->k0 = tz * e1[1];
     rec->k1 = tz * e1[0];
     rec->dz = dz;
+    rec->pad0 = rec->pad1 = 0.0;
 
     const double eps = 1.1102230246251565e-16;  // 2^-53
     const double mnx = fmin(v0[0], fmin(v1[0], v2[0])), mxx = fmax(v0[0], fmax(v1[0], v2[0]));
@@ -428,10 +414,11 @@ __global__ void __launch_bounds__(kThreads) generic_kernel(
 // ---------------------------------------------------------------------------
 // Binned path
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(kThreads) prep_kernel(
+__global__ void __launch_bounds__(kPrepThreads) prep_kernel(
     SceneDev scene, float4 dir, int width, int row_begin, int row_end,
     TriRec* __restrict__ tri, SphRec* __restrict__ sph, int4* __restrict__ boxes,
-    Cls* __restrict__ cls, unsigned* __restrict__ nonfinite_flag, unsigned gen) {
+    Cls* __restrict__ cls, float4* __restrict__ colours, unsigned* __restrict__ nonfinite_flag,
+    unsigned gen, unsigned long long* __restrict__ masks, int n_words, int n_cx) {
     const int n_tri = 12 * scene.n_cubes;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     Box b = empty_box();
@@ -441,19 +428,19 @@ __global__ void __launch_bounds__(kThreads) prep_kernel(
         const float4* v = scene.cube_vertices + 3 * i;
         const float4 a = v[0], bb = v[1], c = v[2];
         const float fa[3] = {a.x, a.y, a.z}, fb[3] = {bb.x, bb.y, bb.z}, fc[3] = {c.x, c.y, c.z};
+        if (i % 12 == 0) colours[i / 12] = scene.cube_colours[i / 12];
         TriRec r{};
         prep_triangle(fa, fb, fc, (double)dir.x, (double)dir.y, (double)dir.z, width, row_begin,
                       row_end, &r, &b, &k, &bad);
-        r.colour = scene.cube_colours[i / 12];
         tri[i] = r;
     } else if (i < n_tri + scene.n_spheres) {
         const int s = i - n_tri;
         const float4 o = scene.sphere_origins[s];
+        colours[scene.n_cubes + s] = scene.sphere_colours[s];
         const float fo[4] = {o.x, o.y, o.z, o.w};
         SphRec r{};
         prep_sphere(fo, scene.sphere_radius[s], dir.x, dir.y, dir.z, dir.w, width, row_begin,
                     row_end, &r, &b, &k, &bad);
-        r.colour = scene.sphere_colours[s];
         sph[s] = r;
     } else {
         return;
@@ -461,37 +448,16 @@ __global__ void __launch_bounds__(kThreads) prep_kernel(
     boxes[i] = make_int4(b.x0, b.y0, b.x1, b.y1);
     cls[i] = k;
     if (bad) atomicMax(nonfinite_flag, gen);
-}
-
-// Coarse binning: one wave per 64x64-pixel coarse bin writes the ordered
-// list of primitives whose box touches it (ballot + mbcnt compaction keeps
-// the reference's primitive order: cubes' triangles, then spheres).
-__global__ void __launch_bounds__(kThreads) coarse_kernel(
-    const int4* __restrict__ boxes, int n_prims, int n_cx, int n_coarse, int row_begin,
-    int cap, int* __restrict__ counts, int* __restrict__ lists) {
-    const int cb = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
-    if (cb >= n_coarse) return;  // wave-uniform
-    const int lane = threadIdx.x & 63;
-    const int x0 = (cb % n_cx) * kCoarse, x1 = x0 + kCoarse - 1;
-    const int y0 = row_begin + (cb / n_cx) * kCoarse, y1 = y0 + kCoarse - 1;
-    int* out = lists + (int64_t)cb * cap;
-    int count = 0;
-    for (int base = 0; base < n_prims; base += 64) {
-        const int p = base + lane;
-        bool ov = false;
-        if (p < n_prims) {
-            const int4 b = boxes[p];
-            ov = b.x <= x1 && b.z >= x0 && b.y <= y1 && b.w >= y0;
-        }
-        const unsigned long long m = __ballot(ov);
-        if (ov) {
-            const unsigned below = __builtin_amdgcn_mbcnt_hi(
-                (unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-            out[count + (int)below] = p;
-        }
-        count += __popcll(m);
+    // Coarse binning by scatter: set bit i of every 64x64 coarse bin the box
+    // touches.  Bit order is the primitive order (cubes' triangles, then
+    // spheres), so the bins' candidate lists come out ordered for free.
+    if (b.x0 <= b.x1 && b.y0 <= b.y1) {
+        const unsigned long long bit = 1ull << (i & 63);
+        const int w = i >> 6;
+        for (int cy = (b.y0 - row_begin) / kCoarse; cy <= (b.y1 - row_begin) / kCoarse; ++cy)
+            for (int cx = b.x0 / kCoarse; cx <= b.x1 / kCoarse; ++cx)
+                atomicOr(&masks[((int64_t)cy * n_cx + cx) * n_words + w], bit);
     }
-    if (lane == 0) counts[cb] = count;
 }
 
 // Per-lane exact tests of one candidate primitive `p` (wave-uniform) on the
@@ -499,12 +465,11 @@ __global__ void __launch_bounds__(kThreads) coarse_kernel(
 // the per-triangle constants (see TriRec); `inside` (wave-uniform) means the
 // tile classifier proved every pixel of the tile passes the u/v tests, so
 // only the exact t is computed.  Spheres: :300-327 on SphRec.
-__device__ __forceinline__ void test_primitive(int p, bool inside, const Cls& k, int n_tri,
-                                               const TriRec* __restrict__ tri,
+__device__ __forceinline__ void test_primitive(int p, int slot, bool inside, const Cls& k,
+                                               int n_tri, const TriRec* __restrict__ tri,
                                                const SphRec* __restrict__ sph, double px,
                                                float pxf, const double* py, const float* pyf,
-                                               float* closest, float* cr, float* cg,
-                                               float* cb) {
+                                               float* closest, int* hit) {
     if (p < n_tri) {
         const TriRec r = tri[p];
         const double tx = px - r.v0x;
@@ -519,9 +484,7 @@ __device__ __forceinline__ void test_primitive(int p, bool inside, const Cls& k,
                 const float tf = (float)t;
                 if (tf < closest[j]) {
                     closest[j] = tf;
-                    cr[j] = r.colour.x;
-                    cg[j] = r.colour.y;
-                    cb[j] = r.colour.z;
+                    hit[j] = slot;
                 }
             }
             return;
@@ -565,9 +528,7 @@ __device__ __forceinline__ void test_primitive(int p, bool inside, const Cls& k,
                 const float tf = (float)t;
                 if (tf < closest[j]) {
                     closest[j] = tf;
-                    cr[j] = r.colour.x;
-                    cg[j] = r.colour.y;
-                    cb[j] = r.colour.z;
+                    hit[j] = slot;
                 }
             }
         }
@@ -585,102 +546,7 @@ __device__ __forceinline__ void test_primitive(int p, bool inside, const Cls& k,
                 const float t0 = s.tca - thc;
                 if (t0 != 0.0f && t0 < closest[j]) {
                     closest[j] = t0;
-                    cr[j] = s.colour.x;
-                    cg[j] = s.colour.y;
-                    cb[j] = s.colour.z;
-                }
-            }
-        }
-    }
-}
-
-__device__ __forceinline__ void test_record(bool is_tri, bool inside, const Cls& k,
-                                            const TriRec& r, double px, float pxf,
-                                            const double* py, const float* pyf, float* closest,
-                                            float* cr, float* cg, float* cb) {
-    if (is_tri) {
-        const double tx = px - r.v0x;
-        if (inside) {
-#pragma unroll
-            for (int j = 0; j < kRowsPerLane; ++j) {
-                const double ty = py[j] - r.v0y;
-                const double q2 = tx * r.e1y - ty * r.e1x;
-                const double q0 = ty * r.e1z - r.k0;
-                const double q1 = r.k1 - tx * r.e1z;
-                const double t = (r.e2x * q0 + r.e2y * q1 + r.e2z * q2) * r.inv_det;
-                const float tf = (float)t;
-                if (tf < closest[j]) {
-                    closest[j] = tf;
-                    cr[j] = r.colour.x;
-                    cg[j] = r.colour.y;
-                    cb[j] = r.colour.z;
-                }
-            }
-            return;
-        }
-        // Partial tile: classify each pixel on the fp32 planes first (same
-        // margin as the tile classifier); only pixels inside the margin band
-        // of an edge run the full fp64 u/v test, proven-inside pixels compute
-        // t only, proven-outside pixels are done.
-#if RT_PIXCLS
-        const float xl = pxf - k.a.x;
-        const float ux = k.a.z * xl, vx = k.b.x * xl;
-        const float g = k.b.z;
-#endif
-#pragma unroll
-        for (int j = 0; j < kRowsPerLane; ++j) {
-#if RT_PIXCLS
-            const float yl = pyf[j] - k.a.y;
-            const float ul = ux + k.a.w * yl;
-            const float vl = vx + k.b.y * yl;
-            const float wl = ul + vl;
-            const bool out = ul < -g || ul > 1.0f + g || vl < -g || vl > 1.0f + g || wl > 1.0f + g;
-            const bool in = ul > g && ul < 1.0f - g && vl > g && vl < 1.0f - g && wl < 1.0f - g;
-            if (out) continue;
-#else
-            const bool in = false;
-#endif
-            const double ty = py[j] - r.v0y;
-            const double q2 = tx * r.e1y - ty * r.e1x;
-            bool pass = in;
-            if (!in) {
-                // u = ((tx*p0 + ty*p1) + tz*p2) * inv_det, tz*p2 == +-0 for d = (0,0,D)
-                const double u = (tx * r.p0 + ty * r.p1) * r.inv_det;
-                // v = ((d0*q0 + d1*q1) + d2*q2) * inv_det, d0 = d1 = +-0
-                const double v = (r.dz * q2) * r.inv_det;
-                pass = !(u < 0.0 || u > 1.0) && !(v < 0.0 || u + v > 1.0);
-            }
-            if (pass) {
-                const double q0 = ty * r.e1z - r.k0;
-                const double q1 = r.k1 - tx * r.e1z;
-                const double t = (r.e2x * q0 + r.e2y * q1 + r.e2z * q2) * r.inv_det;
-                const float tf = (float)t;
-                if (tf < closest[j]) {
-                    closest[j] = tf;
-                    cr[j] = r.colour.x;
-                    cg[j] = r.colour.y;
-                    cb[j] = r.colour.z;
-                }
-            }
-        }
-    } else {
-        SphRec s;
-        __builtin_memcpy(&s, &r, sizeof s);  // spheres share the 128-B slots
-        const float lx = s.cx - pxf;
-        const float lx2 = lx * lx;
-#pragma unroll
-        for (int j = 0; j < kRowsPerLane; ++j) {
-            const float ly = s.cy - pyf[j];
-            const float a = lx2 + ly * ly;
-            const float dist2 = (a + s.kzw) - s.tca2;
-            if (!(dist2 > s.r2)) {
-                const float thc = sqrtf(s.r2 - dist2);
-                const float t0 = s.tca - thc;
-                if (t0 != 0.0f && t0 < closest[j]) {
-                    closest[j] = t0;
-                    cr[j] = s.colour.x;
-                    cg[j] = s.colour.y;
-                    cb[j] = s.colour.z;
+                    hit[j] = slot;
                 }
             }
         }
@@ -725,279 +591,192 @@ __device__ __forceinline__ void store_pixel(void* __restrict__ out, int out_form
         reinterpret_cast<unsigned*>(out)[idx] = pack_rgba8(pix);
 }
 
-#if RT_STAMPS
-// Diagnostics only (never in the shipped build): per-phase wave-cycle sums.
-// [0] stage+barrier [1] filter [2] walk [3] shade [4] store issue [5] waves
-// [6] triangle candidates [7] of which tile-inside [8] sphere candidates
-constexpr int kStampWaves = 1 << 17;  // per-wave slots of one launch
-__device__ unsigned long long g_stamps[kStampWaves * 8];
-#define STAMP(t)                                                                   \
-    do {                                                                           \
-        __builtin_amdgcn_sched_barrier(0);                                         \
-        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory"); \
-        __builtin_amdgcn_sched_barrier(0);                                         \
-    } while (0)
-#else
-#define STAMP(t) do { } while (0)
-#endif
-
-// One workgroup per 64x64 coarse bin (4 waves); each wave renders
-// kTilesPerWave tiles of kWaveTile x kWaveTileH pixels, kRowsPerLane pixels
-// per lane.  The coarse bin's candidate list (ids, boxes, classifiers) is
-// staged in LDS once per workgroup; for each tile the wave filters it (one
-// ballot per 64 entries, compacted in order into a per-wave LDS list with
-// the tile classification in bit 31), walks that list with one flat uniform
-// loop (scalar record loads -> per-lane exact tests; the winning colour
-// travels with `closest`), then shades and stores -- and moves on to the
-// next tile while those stores drain.
+// One workgroup per bin (2x2 wave tiles), kRowsPerLane pixels per lane.
+// The parent coarse bin's candidate list (ids, boxes, classifiers) is staged
+// in LDS once per workgroup; each wave filters it against its own tile (one
+// ballot per 64 entries, compacted in order into a per-wave LDS list with the
+// tile classification in bit 31), then walks that list with one flat uniform
+// loop: scalar record loads -> per-lane exact tests.
 // kMode is a diagnostics ablation (rt_debug_set_trace_mode): 0 = the real
 // kernel, 1 = stores only (the store floor of this exact pattern), 2 = stage
 // and filter candidates but skip the per-pixel tests, 3 = everything but the
-// framebuffer stores, 4 = per-pixel tests against records 0 / n_tri only
-// (wrong pixels; timing only).
-constexpr int kTilesX = kCoarse / kWaveTile, kTilesY = kCoarse / kWaveTileH;
-constexpr int kTilesPerWave = kTilesX * kTilesY / (kTraceThreads / 64);
-static_assert(kTilesPerWave * (kTraceThreads / 64) == kTilesX * kTilesY, "tiles per wave");
-
-#ifndef RT_WPE
-#define RT_WPE 0                  // >0: ask the allocator for this many waves per SIMD
-#endif
+// framebuffer stores, 4 = per-pixel tests without the per-candidate record
+// loads (wrong pixels; timing only).
 template <int kMode>
-__global__ void __launch_bounds__(kTraceThreads)
-#if RT_WPE > 0
-__attribute__((amdgpu_waves_per_eu(RT_WPE)))
-#endif
-trace_kernel(
+__global__ void __launch_bounds__(kThreads) trace_kernel(
     SceneDev scene, const TriRec* __restrict__ tri, const SphRec* __restrict__ sph,
-    const int4* __restrict__ boxes, const Cls* __restrict__ cls, const int* __restrict__ counts,
-    const int* __restrict__ lists, int cap, const unsigned* __restrict__ nonfinite_flag,
-    unsigned gen, float4 dir, int width, int row_begin, int row_end, int n_cx, int out_format,
-    void* __restrict__ out) {
+    const int4* __restrict__ boxes, const Cls* __restrict__ cls,
+    const float4* __restrict__ colours, unsigned long long* __restrict__ masks, int n_words,
+    unsigned* __restrict__ done, const unsigned* __restrict__ nonfinite_flag,
+    unsigned gen, float4 dir, int width, int row_begin, int row_end, int n_bins_x, int n_cx,
+    int out_format, void* __restrict__ out) {
     __shared__ int s_id[kStage];
     __shared__ int4 s_box[kStage];
     __shared__ Cls s_cls[kStage];
-    __shared__ int s_wlist[kTraceThreads / 64][kStage];
-#if RT_LDSREC
-    __shared__ TriRec s_rec[kStage];
-#endif
-    const int coarse = blockIdx.x;
+    __shared__ int s_wlist[kThreads / 64][kStage];
+    __shared__ int s_meta[2];
+    const int bin = blockIdx.x;
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
-    const int block_x = (coarse % n_cx) * kCoarse;
-    const int block_y = row_begin + (coarse / n_cx) * kCoarse;
+    const int bin_x = (bin % n_bins_x) * kBinW;
+    const int bin_y = (bin / n_bins_x) * kBinH;  // relative to row_begin
+    const int tile_x = bin_x + (wave & 1) * kWaveTile;
+    const int tile_y = row_begin + bin_y + (wave >> 1) * kWaveTileH;
+    const int x = tile_x + (lane % kWaveTile);
+    const int y0 = tile_y + (lane / kWaveTile);
     const int n_tri = 12 * scene.n_cubes;
-    const int lx = lane % kWaveTile, ly = lane / kWaveTile;
 
     if (kMode == 0 && *nonfinite_flag == gen) {
         // Non-finite scene data: the algebraic shortcuts of the binned path
         // assume finite values, so run the reference algorithm verbatim.
 #pragma unroll 1
-        for (int k = 0; k < kTilesPerWave; ++k) {
-            const int t = wave + (kTraceThreads / 64) * k;
-            const int x = block_x + (t % kTilesX) * kWaveTile + lx;
-#pragma unroll 1
-            for (int j = 0; j < kRowsPerLane; ++j) {
-                const int y = block_y + (t / kTilesX) * kWaveTileH + ly + kLaneRows * j;
-                if (x >= width || y >= row_end) continue;
-                const int4v p =
-                    collide_generic(scene, make_float4((float)x, (float)y, 0.0f, 1.0f), dir);
-                store_pixel(out, out_format, (int64_t)(y - row_begin) * width + x, p);
-            }
+        for (int j = 0; j < kRowsPerLane; ++j) {
+            const int y = y0 + kLaneRows * j;
+            if (x >= width || y >= row_end) continue;
+            const int4v p =
+                collide_generic(scene, make_float4((float)x, (float)y, 0.0f, 1.0f), dir);
+            store_pixel(out, out_format, (int64_t)(y - row_begin) * width + x, p);
         }
         return;
     }
 
-    unsigned long long st[6] = {0, 0, 0, 0, 0, 0}, ta = 0, tb = 0;
-    unsigned long long n_ct = 0, n_ci = 0, n_cs = 0;
-    (void)st; (void)ta; (void)tb; (void)n_ct; (void)n_ci; (void)n_cs;
-    STAMP(ta);
-    const int count = kMode == 1 ? 0 : counts[coarse];
-    const int* __restrict__ list = lists + (int64_t)coarse * cap;
-    int* wlist = s_wlist[wave];
-    const bool one_stage = count <= kStage;
+    float closest[kRowsPerLane];
+    int hit[kRowsPerLane];  // colour slot of the closest primitive, -1 = none
+    double py[kRowsPerLane];
+    float pyf[kRowsPerLane];
+#pragma unroll
+    for (int j = 0; j < kRowsPerLane; ++j) {
+        closest[j] = kFar;
+        hit[j] = -1;
+        py[j] = (double)(y0 + kLaneRows * j);
+        pyf[j] = (float)(y0 + kLaneRows * j);
+    }
+    const double px = (double)x;
+    const float pxf = (float)x;
+    const int tx1 = tile_x + kWaveTile - 1, ty1 = tile_y + kWaveTileH - 1;
 
-    auto stage = [&](int s0, int n) {
-        for (int i = threadIdx.x; i < n; i += kTraceThreads) {
-            const int id = list[s0 + i];
-            s_id[i] = id;
+    // The coarse bin's mask words: expanded into ordered ids in LDS, at most
+    // kStage ids per stage (whole words; a word holds <= 64 ids).
+    const int cb = (bin_y / kCoarse) * n_cx + bin_x / kCoarse;
+    unsigned long long* cmask = masks + (int64_t)cb * n_words;
+    int* wlist = s_wlist[wave];
+    int w_next = 0;  // first mask word not yet staged (workgroup-uniform)
+    bool first = true;
+    while (kMode != 1 && w_next < n_words) {
+        if (!first) __syncthreads();  // previous stage fully consumed
+        first = false;
+        if (wave == 0) {
+            // one wave: popcounts of the next 64 words, inclusive scan, take
+            // the longest prefix of words with <= kStage ids (at least one)
+            const int wi = w_next + lane;
+            const unsigned long long m = wi < n_words ? cmask[wi] : 0ull;
+            int c = __popcll(m), incl = c;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const int o = __shfl_up(incl, d);
+                if (lane >= d) incl += o;
+            }
+            const unsigned long long fits = __ballot(wi < n_words && incl <= kStage);
+            const int take = fits ? 64 - __builtin_clzll(fits) : 1;  // words in this stage
+            if (lane < take && c) {
+                int k = incl - c;
+                unsigned long long mm = m;
+                while (mm) {
+                    s_id[k++] = wi * 64 + __builtin_ctzll(mm);
+                    mm &= mm - 1;
+                }
+            }
+            if (lane == 0) {
+                s_meta[0] = __shfl(incl, take - 1);  // ids in this stage
+                s_meta[1] = w_next + take;
+            }
+        }
+        __syncthreads();
+        const int n = s_meta[0];
+        w_next = s_meta[1];
+        for (int i = threadIdx.x; i < n; i += kThreads) {
+            const int id = s_id[i];
             s_box[i] = boxes[id];
             s_cls[i] = cls[id];
         }
-#if RT_LDSREC
-        // candidate records, 16 B per lane (spheres: the 48-B SphRec)
-        for (int i = threadIdx.x; i < n * 8; i += kTraceThreads) {
-            const int id = list[s0 + (i >> 3)];
-            const int part = i & 7;
-            float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            if (id < n_tri)
-                v = reinterpret_cast<const float4*>(tri + id)[part];
-            else if (part < 3)
-                v = reinterpret_cast<const float4*>(sph + (id - n_tri))[part];
-            reinterpret_cast<float4*>(s_rec)[i] = v;
-        }
-#endif
-    };
-    if (one_stage && count > 0) {
-        stage(0, count);
         __syncthreads();
-    }
-    STAMP(tb);
-#if RT_STAMPS
-    st[0] += tb - ta;
-    ta = tb;
-#endif
-
-#pragma unroll 1
-    for (int k = 0; k < kTilesPerWave; ++k) {
-        const int t = wave + (kTraceThreads / 64) * k;
-        const int tile_x = block_x + (t % kTilesX) * kWaveTile;
-        const int tile_y = block_y + (t / kTilesX) * kWaveTileH;
-        // tiles wholly outside the frame / band (uniform; no barriers follow
-        // on the one-stage path, so skipping is safe there)
-        if (one_stage && (tile_x >= width || tile_y >= row_end)) continue;
-        const int x = tile_x + lx;
-        const int y0 = tile_y + ly;
-        const int tx1 = tile_x + kWaveTile - 1, ty1 = tile_y + kWaveTileH - 1;
-
-        float closest[kRowsPerLane];  // kFar = no hit (a hit always sets closest < kFar)
-        float cr[kRowsPerLane], cg[kRowsPerLane], cb[kRowsPerLane];  // its colour
-        double py[kRowsPerLane];
-        float pyf[kRowsPerLane];
-#pragma unroll
-        for (int j = 0; j < kRowsPerLane; ++j) {
-            closest[j] = kFar;
-            cr[j] = cg[j] = cb[j] = 0.0f;
-            py[j] = (double)(y0 + kLaneRows * j);
-            pyf[j] = (float)(y0 + kLaneRows * j);
-        }
-        const double px = (double)x;
-        const float pxf = (float)x;
-
-        for (int s0 = 0; s0 < count; s0 += kStage) {
-            const int n = min(kStage, count - s0);
-            if (!one_stage) {  // uniform across the workgroup
-                __syncthreads();
-                stage(s0, n);
-                __syncthreads();
-            }
-            // filter: this wave's candidates for this tile, in order
-            int wn = 0;
-            for (int c = 0; c < n; c += 64) {
-                const int e = c + lane;
-                bool keep = false, inside = false;
-                int id = 0;
-                if (e < n) {
-                    const int4 b = s_box[e];
-                    id = s_id[e];
-                    if (b.x <= tx1 && b.z >= tile_x && b.y <= ty1 && b.w >= tile_y) {
+        // filter: this wave's candidates, in order, into wlist
+        int wn = 0;
+        for (int c = 0; c < n; c += 64) {
+            const int e = c + lane;
+            bool keep = false, inside = false;
+            int id = 0;
+            if (e < n) {
+                const int4 b = s_box[e];
+                id = s_id[e];
+                if (b.x <= tx1 && b.z >= tile_x && b.y <= ty1 && b.w >= tile_y) {
 #if RT_TILECLS
-                        classify(s_cls[e], id < n_tri, (float)tile_x, (float)tile_y, &keep,
-                                 &inside);
+                    classify(s_cls[e], id < n_tri, (float)tile_x, (float)tile_y, &keep, &inside);
 #else
-                        keep = true;
-#endif
-                    }
-                }
-                const unsigned long long m = __ballot(keep);
-                if (keep) {
-                    const unsigned below = __builtin_amdgcn_mbcnt_hi(
-                        (unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-#if RT_LDSREC
-                    wlist[wn + (int)below] = e | (id < n_tri ? 0x40000000 : 0) |
-                                             (inside ? (int)0x80000000u : 0);
-#else
-                    wlist[wn + (int)below] = id | (inside ? (int)0x80000000u : 0);
+                    keep = true;
 #endif
                 }
-                wn += __popcll(m);
             }
-            // wlist was written by other lanes of this wave: LDS ops of one
-            // wave complete in order, so waiting on lgkmcnt (not a release
-            // fence, which would also wait for the previous tile's stores)
-            // and a compiler barrier suffice.
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            STAMP(tb);
-#if RT_STAMPS
-            st[1] += tb - ta;
-            ta = tb;
-#endif
-#if RT_LDSREC
-            for (int i = 0; i < wn && kMode != 2; ++i) {
-                const int v = __builtin_amdgcn_readfirstlane(wlist[i]);
-                const int e = v & 0x3fffffff;
-                const TriRec r = s_rec[kMode == 4 ? 0 : e];
-                test_record((v & 0x40000000) != 0, v < 0, Cls{}, r, px, pxf, py, pyf, closest,
-                            cr, cg, cb);
+            const unsigned long long m = __ballot(keep);
+            if (keep) {
+                const unsigned below = __builtin_amdgcn_mbcnt_hi(
+                    (unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+                wlist[wn + (int)below] = id | (inside ? (int)0x80000000u : 0);
             }
-            for (int i = 0; i < wn && kMode == 2; ++i) {
-#else
-            for (int i = 0; i < wn; ++i) {
-#endif
-                const int v = __builtin_amdgcn_readfirstlane(wlist[i]);
-                const int p = v & 0x7fffffff;
-                if (kMode == 2) {
-                    cr[0] = cr[0] > (float)p ? cr[0] : 0.0f;  // keep the walk alive
-                    continue;
-                }
-#if RT_STAMPS
-                n_ct += p < n_tri;
-                n_ci += p < n_tri && v < 0;
-                n_cs += p >= n_tri;
-#endif
-#if !RT_LDSREC
-                const int pr = kMode == 4 ? (p < n_tri ? 0 : n_tri) : p;
-                test_primitive(pr, v < 0, Cls{}, n_tri, tri, sph, px, pxf, py, pyf, closest, cr,
-                               cg, cb);
-#endif
-            }
-            STAMP(tb);
-#if RT_STAMPS
-            st[2] += tb - ta;
-            ta = tb;
-#endif
+            wn += __popcll(m);
         }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (int i = 0; i < wn; ++i) {
+            const int v = __builtin_amdgcn_readfirstlane(wlist[i]);
+            const int p = v & 0x7fffffff;
+            if (kMode == 2) {
+                hit[0] = hit[0] > p ? hit[0] : -1;  // keep the walk alive
+                continue;
+            }
+            const int slot = p < n_tri ? p / 12 : scene.n_cubes + (p - n_tri);
+            // kMode 4: same tests on record 0 / sphere 0 (no dependent record loads)
+            const int pr = kMode == 4 ? (p < n_tri ? 0 : n_tri) : p;
+            test_primitive(pr, slot, v < 0, Cls{}, n_tri, tri, sph, px, pxf, py, pyf, closest,
+                           hit);
+        }
+    }
 
-        // Shade + store.  The winning colour travelled with closest (scalar-
-        // loaded with each candidate's record), so shading touches no memory.
-        int4v pix[kRowsPerLane];
-#pragma unroll
-        for (int j = 0; j < kRowsPerLane; ++j) {
-            pix[j] = int4v{0, 0, 0, 255};
-            if (closest[j] != kFar)
-                pix[j] = shade_hit(closest[j], make_float4(cr[j], cg[j], cb[j], 0.0f));
+    // The last of the workgroups sharing this coarse bin to finish reading
+    // its mask words zeroes them (and the arrival counter), so every frame
+    // ends with all masks clear for the next prep.
+    if (wave == 0) {
+        const int kcx = kCoarse / kBinW, kcy = kCoarse / kBinH;
+        const int cbx = cb % n_cx, cby = cb / n_cx;
+        const int n_bins_y = (row_end - row_begin + kBinH - 1) / kBinH;
+        const unsigned share = (unsigned)(min(kcx, n_bins_x - cbx * kcx) *
+                                          min(kcy, n_bins_y - cby * kcy));
+        unsigned old = 0;
+        if (lane == 0) old = atomicAdd(&done[cb], 1u);
+        old = __shfl(old, 0);
+        if (old == share - 1) {
+            for (int w = lane; w < n_words; w += 64) cmask[w] = 0ull;
+            if (lane == 0) done[cb] = 0u;
         }
-#if RT_STAMPS
-        asm volatile("" ::"v"(pix[0].x), "v"(pix[kRowsPerLane - 1].z));
-#endif
-        STAMP(tb);
-#if RT_STAMPS
-        st[3] += tb - ta;
-        ta = tb;
-#endif
+    }
+
+    // Shade + store.  A wave whose pixels all missed (ballot) stores the
+    // black pattern without touching the colour table.
+    bool lane_hit = false;
 #pragma unroll
-        for (int j = 0; j < kRowsPerLane; ++j) {
-            const int y = y0 + kLaneRows * j;
-            // kMode 3: everything but the stores (a store the compiler cannot drop)
-            const bool store = kMode != 3 || pix[j].x == 0x7fffffff;
-            if (x < width && y < row_end && store)
-                store_pixel(out, out_format, (int64_t)(y - row_begin) * width + x, pix[j]);
-        }
-        STAMP(tb);
-#if RT_STAMPS
-        st[4] += tb - ta;
-        ta = tb;
-#endif
+    for (int j = 0; j < kRowsPerLane; ++j) lane_hit |= hit[j] >= 0;
+    const bool any_hit = __ballot(lane_hit) != 0ull;
+#pragma unroll
+    for (int j = 0; j < kRowsPerLane; ++j) {
+        const int y = y0 + kLaneRows * j;
+        int4v pix{0, 0, 0, 255};
+        if (any_hit && hit[j] >= 0) pix = shade_hit(closest[j], colours[hit[j]]);
+        // kMode 3: everything but the stores (a store the compiler cannot drop)
+        const bool store = kMode != 3 || pix.x == 0x7fffffff;
+        if (x < width && y < row_end && store)
+            store_pixel(out, out_format, (int64_t)(y - row_begin) * width + x, pix);
     }
-#if RT_STAMPS
-    const int gw = blockIdx.x * (kTraceThreads / 64) + wave;
-    if (lane == 0 && gw < kStampWaves) {  // plain per-wave stores (no contention)
-        unsigned long long* slot = g_stamps + (size_t)gw * 8;
-        for (int k = 0; k < 5; ++k) slot[k] = st[k];
-        slot[5] = 1;
-        slot[6] = n_ct;
-        slot[7] = n_ci | (n_cs << 32);
-    }
-#endif
 }
 
 // fp32 self-test: the device's sqrtf and '/' must be correctly rounded.
@@ -1021,7 +800,7 @@ struct rt_ctx {
     void* origin_buf = nullptr; size_t origin_cap = 0;  // host-API explicit origins
     void* out_buf = nullptr;    size_t out_cap = 0;     // host-API frame
     void* rec_buf = nullptr;    size_t rec_cap = 0;     // TriRec/SphRec/boxes/flag
-    void* list_buf = nullptr;   size_t list_cap = 0;    // coarse-bin candidate lists
+    void* mask_buf = nullptr;   size_t mask_cap = 0;    // coarse-bin masks + counters
     unsigned* flag = nullptr;   // non-finite scene flag (generation-stamped)
     unsigned gen = 0;
     int trace_mode = 0;  // diagnostics ablation, see trace_kernel
@@ -1119,31 +898,44 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
     }
     const int n_tri = 12 * s->num_cubes;
     const int n_prims = n_tri + s->num_spheres;
+    const int n_bins_x = (width + kBinW - 1) / kBinW;
+    const int n_bins_y = (rows + kBinH - 1) / kBinH;
     const int n_cx = (width + kCoarse - 1) / kCoarse;
     const int n_cy = (rows + kCoarse - 1) / kCoarse;
+    const int64_t n_bins64 = (int64_t)n_bins_x * n_bins_y;
     const int64_t n_coarse64 = (int64_t)n_cx * n_cy;
-    if (n_coarse64 >= (int64_t)1 << 31) return RT_ERR_INVALID_ARG;
+    if (n_bins64 >= (int64_t)1 << 31) return RT_ERR_INVALID_ARG;
+    const int n_bins = (int)n_bins64;
     const int n_coarse = (int)n_coarse64;
-    const int cap = n_prims > 0 ? n_prims : 1;
+    const int n_words = (n_prims + 63) / 64;
 
     const size_t tri_off = 0;
     const size_t sph_off = align_up(sizeof(TriRec) * (size_t)n_tri, 256);
     const size_t box_off = sph_off + align_up(sizeof(SphRec) * (size_t)s->num_spheres, 256);
     const size_t cls_off = box_off + align_up(sizeof(int4) * (size_t)n_prims, 256);
-    const size_t cnt_off = cls_off + align_up(sizeof(Cls) * (size_t)n_prims, 256);
-    const size_t rec_need = cnt_off + align_up(sizeof(int) * (size_t)n_coarse, 256);
+    const size_t col_off = cls_off + align_up(sizeof(Cls) * (size_t)n_prims, 256);
+    const size_t rec_need =
+        col_off + align_up(sizeof(float4) * (size_t)(s->num_cubes + s->num_spheres), 256);
     int rc = ensure(&ctx->rec_buf, &ctx->rec_cap, rec_need);
     if (rc) return rc;
-    const size_t list_need = sizeof(int) * (size_t)cap * (size_t)n_coarse + 256;
-    rc = ensure(&ctx->list_buf, &ctx->list_cap, list_need);
-    if (rc) return rc;
+    // coarse-bin masks + arrival counters: zero on allocation, and every
+    // frame's trace kernel leaves them zero again (see trace_kernel)
+    const size_t mask_bytes = sizeof(unsigned long long) * (size_t)n_words * (size_t)n_coarse;
+    const size_t mask_need = align_up(mask_bytes, 256) + sizeof(unsigned) * (size_t)n_coarse + 256;
+    if (mask_need > ctx->mask_cap) {
+        rc = ensure(&ctx->mask_buf, &ctx->mask_cap, mask_need);
+        if (rc) return rc;
+        HIP_TRY(hipMemsetAsync(ctx->mask_buf, 0, ctx->mask_cap, stream));
+    }
     char* base = static_cast<char*>(ctx->rec_buf);
     TriRec* tri = reinterpret_cast<TriRec*>(base + tri_off);
     SphRec* sph = reinterpret_cast<SphRec*>(base + sph_off);
     int4* boxes = reinterpret_cast<int4*>(base + box_off);
     Cls* clsv = reinterpret_cast<Cls*>(base + cls_off);
-    int* counts = reinterpret_cast<int*>(base + cnt_off);
-    int* lists = static_cast<int*>(ctx->list_buf);
+    float4* colours = reinterpret_cast<float4*>(base + col_off);
+    auto* masks = static_cast<unsigned long long*>(ctx->mask_buf);
+    auto* done = reinterpret_cast<unsigned*>(static_cast<char*>(ctx->mask_buf) +
+                                             align_up(mask_bytes, 256));
     // generation-stamped non-finite flag: no per-launch memset needed
     if (++ctx->gen == 0) {
         HIP_TRY(hipMemsetAsync(ctx->flag, 0, sizeof(unsigned), stream));
@@ -1151,22 +943,22 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
     }
 
     if (n_prims > 0) {
-        prep_kernel<<<dim3((n_prims + kThreads - 1) / kThreads), dim3(kThreads), 0, stream>>>(
-            sd, dir, width, row_begin, row_end, tri, sph, boxes, clsv, ctx->flag, ctx->gen);
+        prep_kernel<<<dim3((n_prims + kPrepThreads - 1) / kPrepThreads), dim3(kPrepThreads), 0,
+                      stream>>>(sd, dir, width, row_begin, row_end, tri, sph, boxes, clsv,
+                                colours, ctx->flag, ctx->gen, masks, n_words, n_cx);
         HIP_TRY(hipGetLastError());
     }
-    if (pe) HIP_TRY(hipEventRecord(pe[1], stream));
-    coarse_kernel<<<dim3((n_coarse + 3) / 4), dim3(kThreads), 0, stream>>>(
-        boxes, n_prims, n_cx, n_coarse, row_begin, cap, counts, lists);
-    HIP_TRY(hipGetLastError());
-    if (pe) HIP_TRY(hipEventRecord(pe[2], stream));
+    if (pe) {
+        HIP_TRY(hipEventRecord(pe[1], stream));
+        HIP_TRY(hipEventRecord(pe[2], stream));
+    }
     auto kern = ctx->trace_mode == 1 ? trace_kernel<1>
               : ctx->trace_mode == 2 ? trace_kernel<2>
               : ctx->trace_mode == 3 ? trace_kernel<3>
               : ctx->trace_mode == 4 ? trace_kernel<4> : trace_kernel<0>;
-    kern<<<dim3((unsigned)n_coarse), dim3(kTraceThreads), 0, stream>>>(
-        sd, tri, sph, boxes, clsv, counts, lists, cap, ctx->flag, ctx->gen, dir, width, row_begin,
-        row_end, n_cx, fmt, out);
+    kern<<<dim3((unsigned)n_bins), dim3(kThreads), 0, stream>>>(
+        sd, tri, sph, boxes, clsv, colours, masks, n_words, done, ctx->flag, ctx->gen, dir, width,
+        row_begin, row_end, n_bins_x, n_cx, fmt, out);
     HIP_TRY(hipGetLastError());
     if (pe) HIP_TRY(hipEventRecord(pe[3], stream));
     return RT_OK;
@@ -1220,7 +1012,7 @@ void rt_destroy(rt_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-    for (void* p : {ctx->scene_buf, ctx->origin_buf, ctx->out_buf, ctx->rec_buf, ctx->list_buf,
+    for (void* p : {ctx->scene_buf, ctx->origin_buf, ctx->out_buf, ctx->rec_buf, ctx->mask_buf,
                     static_cast<void*>(ctx->flag)})
         if (p) (void)hipFree(p);
     for (auto& e : ctx->ev)
@@ -1396,31 +1188,6 @@ int rt_debug_triangle_box(const float v0[3], const float v1[3], const float v2[3
     box_out[0] = b.x0; box_out[1] = b.y0; box_out[2] = b.x1; box_out[3] = b.y1;
     if (cls_out) std::memcpy(cls_out, &k, sizeof k);
     return ok ? 1 : 0;
-}
-
-// Diagnostics: read and reset the stamp sums of an RT_STAMPS build (returns
-// RT_ERR_UNSUPPORTED otherwise).
-int rt_debug_read_stamps(rt_ctx* ctx, unsigned long long out[16]) {
-    if (!ctx || !out) return RT_ERR_INVALID_ARG;
-#if RT_STAMPS
-    HIP_TRY(hipSetDevice(ctx->device));
-    HIP_TRY(hipDeviceSynchronize());
-    std::vector<unsigned long long> h((size_t)kStampWaves * 8);
-    HIP_TRY(hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(g_stamps), h.size() * 8));
-    for (int k = 0; k < 16; ++k) out[k] = 0;
-    for (size_t w = 0; w < (size_t)kStampWaves; ++w) {
-        const unsigned long long* v = &h[w * 8];
-        for (int k = 0; k < 6; ++k) out[k] += v[k];
-        out[6] += v[6];
-        out[7] += v[7] & 0xffffffffull;
-        out[8] += v[7] >> 32;
-    }
-    std::vector<unsigned long long> z(h.size(), 0);
-    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z.data(), z.size() * 8));
-    return RT_OK;
-#else
-    return RT_ERR_UNSUPPORTED;
-#endif
 }
 
 // Diagnostics: select a trace-kernel ablation (0 = normal).
