@@ -686,8 +686,9 @@ __global__ void __launch_bounds__(kThreads) trace_kernel(
                     mm &= mm - 1;
                 }
             }
+            const int n_ids = __shfl(incl, take - 1);  // all lanes active here
             if (lane == 0) {
-                s_meta[0] = __shfl(incl, take - 1);  // ids in this stage
+                s_meta[0] = n_ids;  // ids in this stage
                 s_meta[1] = w_next + take;
             }
         }
