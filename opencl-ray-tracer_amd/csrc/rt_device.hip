@@ -678,12 +678,18 @@ __global__ void __launch_bounds__(kThreads) trace_kernel(
             }
             const unsigned long long fits = __ballot(wi < n_words && incl <= kStage);
             const int take = fits ? 64 - __builtin_clzll(fits) : 1;  // words in this stage
-            if (lane < take && c) {
-                int k = incl - c;
-                unsigned long long mm = m;
-                while (mm) {
-                    s_id[k++] = wi * 64 + __builtin_ctzll(mm);
-                    mm &= mm - 1;
+            // word by word, every lane places its own bit (mbcnt compaction)
+            const unsigned lo = (unsigned)m, hi = (unsigned)(m >> 32);
+            const int excl = incl - c;
+            for (int k = 0; k < take; ++k) {
+                const unsigned klo = __builtin_amdgcn_readlane(lo, k);
+                const unsigned khi = __builtin_amdgcn_readlane(hi, k);
+                const int off = __builtin_amdgcn_readlane(excl, k);
+                const unsigned long long mk = ((unsigned long long)khi << 32) | klo;
+                if ((mk >> lane) & 1ull) {
+                    const unsigned below =
+                        __builtin_amdgcn_mbcnt_hi(khi, __builtin_amdgcn_mbcnt_lo(klo, 0u));
+                    s_id[off + (int)below] = (w_next + k) * 64 + lane;
                 }
             }
             const int n_ids = __shfl(incl, take - 1);  // all lanes active here
