@@ -418,7 +418,7 @@ __global__ void __launch_bounds__(kPrepThreads) prep_kernel(
     SceneDev scene, float4 dir, int width, int row_begin, int row_end,
     TriRec* __restrict__ tri, SphRec* __restrict__ sph, int4* __restrict__ boxes,
     Cls* __restrict__ cls, float4* __restrict__ colours, unsigned* __restrict__ nonfinite_flag,
-    unsigned gen, unsigned long long* __restrict__ masks, int n_words, int n_cx) {
+    unsigned gen) {
     const int n_tri = 12 * scene.n_cubes;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     Box b = empty_box();
@@ -448,16 +448,45 @@ __global__ void __launch_bounds__(kPrepThreads) prep_kernel(
     boxes[i] = make_int4(b.x0, b.y0, b.x1, b.y1);
     cls[i] = k;
     if (bad) atomicMax(nonfinite_flag, gen);
-    // Coarse binning by scatter: set bit i of every 64x64 coarse bin the box
-    // touches.  Bit order is the primitive order (cubes' triangles, then
-    // spheres), so the bins' candidate lists come out ordered for free.
-    if (b.x0 <= b.x1 && b.y0 <= b.y1) {
-        const unsigned long long bit = 1ull << (i & 63);
-        const int w = i >> 6;
-        for (int cy = (b.y0 - row_begin) / kCoarse; cy <= (b.y1 - row_begin) / kCoarse; ++cy)
-            for (int cx = b.x0 / kCoarse; cx <= b.x1 / kCoarse; ++cx)
-                atomicOr(&masks[((int64_t)cy * n_cx + cx) * n_words + w], bit);
+}
+
+// Coarse binning: one wave per 64x64-pixel coarse bin writes the ordered
+// list of primitives whose box touches it (ballot + mbcnt compaction keeps
+// the reference's primitive order: cubes' triangles, then spheres).
+__global__ void __launch_bounds__(kThreads) coarse_kernel(
+    const int4* __restrict__ boxes, int n_prims, int n_cx, int n_coarse, int row_begin,
+    int cap, int* __restrict__ counts, int* __restrict__ lists) {
+    const int cb = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+    if (cb >= n_coarse) return;  // wave-uniform
+    const int lane = threadIdx.x & 63;
+    const int x0 = (cb % n_cx) * kCoarse, x1 = x0 + kCoarse - 1;
+    const int y0 = row_begin + (cb / n_cx) * kCoarse, y1 = y0 + kCoarse - 1;
+    int* out = lists + (int64_t)cb * cap;
+    int count = 0;
+    // boxes are loaded kBatch chunks at a time so the loads overlap (the
+    // loop is otherwise a chain of dependent L2 round trips)
+    constexpr int kBatch = 8;
+    for (int base = 0; base < n_prims; base += 64 * kBatch) {
+        int4 bb[kBatch];
+#pragma unroll
+        for (int k = 0; k < kBatch; ++k) {
+            const int p = base + 64 * k + lane;
+            bb[k] = p < n_prims ? boxes[p] : make_int4(1 << 30, 1 << 30, -(1 << 30), -(1 << 30));
+        }
+#pragma unroll
+        for (int k = 0; k < kBatch; ++k) {
+            const int4 b = bb[k];
+            const bool ov = b.x <= x1 && b.z >= x0 && b.y <= y1 && b.w >= y0;
+            const unsigned long long m = __ballot(ov);
+            if (ov) {
+                const unsigned below = __builtin_amdgcn_mbcnt_hi(
+                    (unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+                out[count + (int)below] = base + 64 * k + lane;
+            }
+            count += __popcll(m);
+        }
     }
+    if (lane == 0) counts[cb] = count;
 }
 
 // Per-lane exact tests of one candidate primitive `p` (wave-uniform) on the
@@ -606,15 +635,14 @@ template <int kMode>
 __global__ void __launch_bounds__(kThreads) trace_kernel(
     SceneDev scene, const TriRec* __restrict__ tri, const SphRec* __restrict__ sph,
     const int4* __restrict__ boxes, const Cls* __restrict__ cls,
-    const float4* __restrict__ colours, unsigned long long* __restrict__ masks, int n_words,
-    unsigned* __restrict__ done, const unsigned* __restrict__ nonfinite_flag,
+    const float4* __restrict__ colours, const int* __restrict__ counts,
+    const int* __restrict__ lists, int cap, const unsigned* __restrict__ nonfinite_flag,
     unsigned gen, float4 dir, int width, int row_begin, int row_end, int n_bins_x, int n_cx,
     int out_format, void* __restrict__ out) {
     __shared__ int s_id[kStage];
     __shared__ int4 s_box[kStage];
     __shared__ Cls s_cls[kStage];
     __shared__ int s_wlist[kThreads / 64][kStage];
-    __shared__ int s_meta[2];
     const int bin = blockIdx.x;
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
@@ -655,54 +683,16 @@ __global__ void __launch_bounds__(kThreads) trace_kernel(
     const float pxf = (float)x;
     const int tx1 = tile_x + kWaveTile - 1, ty1 = tile_y + kWaveTileH - 1;
 
-    // The coarse bin's mask words: expanded into ordered ids in LDS, at most
-    // kStage ids per stage (whole words; a word holds <= 64 ids).
     const int cb = (bin_y / kCoarse) * n_cx + bin_x / kCoarse;
-    unsigned long long* cmask = masks + (int64_t)cb * n_words;
+    const int count = kMode == 1 ? 0 : counts[cb];
+    const int* __restrict__ list = lists + (int64_t)cb * cap;
     int* wlist = s_wlist[wave];
-    int w_next = 0;  // first mask word not yet staged (workgroup-uniform)
-    bool first = true;
-    while (kMode != 1 && w_next < n_words) {
-        if (!first) __syncthreads();  // previous stage fully consumed
-        first = false;
-        if (wave == 0) {
-            // one wave: popcounts of the next 64 words, inclusive scan, take
-            // the longest prefix of words with <= kStage ids (at least one)
-            const int wi = w_next + lane;
-            const unsigned long long m = wi < n_words ? cmask[wi] : 0ull;
-            int c = __popcll(m), incl = c;
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const int o = __shfl_up(incl, d);
-                if (lane >= d) incl += o;
-            }
-            const unsigned long long fits = __ballot(wi < n_words && incl <= kStage);
-            const int take = fits ? 64 - __builtin_clzll(fits) : 1;  // words in this stage
-            // word by word, every lane places its own bit (mbcnt compaction)
-            const unsigned lo = (unsigned)m, hi = (unsigned)(m >> 32);
-            const int excl = incl - c;
-            for (int k = 0; k < take; ++k) {
-                const unsigned klo = __builtin_amdgcn_readlane(lo, k);
-                const unsigned khi = __builtin_amdgcn_readlane(hi, k);
-                const int off = __builtin_amdgcn_readlane(excl, k);
-                const unsigned long long mk = ((unsigned long long)khi << 32) | klo;
-                if ((mk >> lane) & 1ull) {
-                    const unsigned below =
-                        __builtin_amdgcn_mbcnt_hi(khi, __builtin_amdgcn_mbcnt_lo(klo, 0u));
-                    s_id[off + (int)below] = (w_next + k) * 64 + lane;
-                }
-            }
-            const int n_ids = __shfl(incl, take - 1);  // all lanes active here
-            if (lane == 0) {
-                s_meta[0] = n_ids;  // ids in this stage
-                s_meta[1] = w_next + take;
-            }
-        }
-        __syncthreads();
-        const int n = s_meta[0];
-        w_next = s_meta[1];
+    for (int s0 = 0; s0 < count; s0 += kStage) {
+        const int n = min(kStage, count - s0);
+        if (s0 > 0) __syncthreads();  // previous stage fully consumed
         for (int i = threadIdx.x; i < n; i += kThreads) {
-            const int id = s_id[i];
+            const int id = list[s0 + i];
+            s_id[i] = id;
             s_box[i] = boxes[id];
             s_cls[i] = cls[id];
         }
@@ -750,24 +740,6 @@ __global__ void __launch_bounds__(kThreads) trace_kernel(
         }
     }
 
-    // The last of the workgroups sharing this coarse bin to finish reading
-    // its mask words zeroes them (and the arrival counter), so every frame
-    // ends with all masks clear for the next prep.
-    if (wave == 0) {
-        const int kcx = kCoarse / kBinW, kcy = kCoarse / kBinH;
-        const int cbx = cb % n_cx, cby = cb / n_cx;
-        const int n_bins_y = (row_end - row_begin + kBinH - 1) / kBinH;
-        const unsigned share = (unsigned)(min(kcx, n_bins_x - cbx * kcx) *
-                                          min(kcy, n_bins_y - cby * kcy));
-        unsigned old = 0;
-        if (lane == 0) old = atomicAdd(&done[cb], 1u);
-        old = __shfl(old, 0);
-        if (old == share - 1) {
-            for (int w = lane; w < n_words; w += 64) cmask[w] = 0ull;
-            if (lane == 0) done[cb] = 0u;
-        }
-    }
-
     // Shade + store.  A wave whose pixels all missed (ballot) stores the
     // black pattern without touching the colour table.
     bool lane_hit = false;
@@ -807,7 +779,7 @@ struct rt_ctx {
     void* origin_buf = nullptr; size_t origin_cap = 0;  // host-API explicit origins
     void* out_buf = nullptr;    size_t out_cap = 0;     // host-API frame
     void* rec_buf = nullptr;    size_t rec_cap = 0;     // TriRec/SphRec/boxes/flag
-    void* mask_buf = nullptr;   size_t mask_cap = 0;    // coarse-bin masks + counters
+    void* list_buf = nullptr;   size_t list_cap = 0;    // coarse-bin candidate lists
     unsigned* flag = nullptr;   // non-finite scene flag (generation-stamped)
     unsigned gen = 0;
     int trace_mode = 0;  // diagnostics ablation, see trace_kernel
@@ -914,35 +886,29 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
     if (n_bins64 >= (int64_t)1 << 31) return RT_ERR_INVALID_ARG;
     const int n_bins = (int)n_bins64;
     const int n_coarse = (int)n_coarse64;
-    const int n_words = (n_prims + 63) / 64;
+    const int cap = n_prims > 0 ? n_prims : 1;
 
     const size_t tri_off = 0;
     const size_t sph_off = align_up(sizeof(TriRec) * (size_t)n_tri, 256);
     const size_t box_off = sph_off + align_up(sizeof(SphRec) * (size_t)s->num_spheres, 256);
     const size_t cls_off = box_off + align_up(sizeof(int4) * (size_t)n_prims, 256);
     const size_t col_off = cls_off + align_up(sizeof(Cls) * (size_t)n_prims, 256);
-    const size_t rec_need =
+    const size_t cnt_off =
         col_off + align_up(sizeof(float4) * (size_t)(s->num_cubes + s->num_spheres), 256);
+    const size_t rec_need = cnt_off + align_up(sizeof(int) * (size_t)n_coarse, 256);
     int rc = ensure(&ctx->rec_buf, &ctx->rec_cap, rec_need);
     if (rc) return rc;
-    // coarse-bin masks + arrival counters: zero on allocation, and every
-    // frame's trace kernel leaves them zero again (see trace_kernel)
-    const size_t mask_bytes = sizeof(unsigned long long) * (size_t)n_words * (size_t)n_coarse;
-    const size_t mask_need = align_up(mask_bytes, 256) + sizeof(unsigned) * (size_t)n_coarse + 256;
-    if (mask_need > ctx->mask_cap) {
-        rc = ensure(&ctx->mask_buf, &ctx->mask_cap, mask_need);
-        if (rc) return rc;
-        HIP_TRY(hipMemsetAsync(ctx->mask_buf, 0, ctx->mask_cap, stream));
-    }
+    const size_t list_need = sizeof(int) * (size_t)cap * (size_t)n_coarse + 256;
+    rc = ensure(&ctx->list_buf, &ctx->list_cap, list_need);
+    if (rc) return rc;
     char* base = static_cast<char*>(ctx->rec_buf);
     TriRec* tri = reinterpret_cast<TriRec*>(base + tri_off);
     SphRec* sph = reinterpret_cast<SphRec*>(base + sph_off);
     int4* boxes = reinterpret_cast<int4*>(base + box_off);
     Cls* clsv = reinterpret_cast<Cls*>(base + cls_off);
     float4* colours = reinterpret_cast<float4*>(base + col_off);
-    auto* masks = static_cast<unsigned long long*>(ctx->mask_buf);
-    auto* done = reinterpret_cast<unsigned*>(static_cast<char*>(ctx->mask_buf) +
-                                             align_up(mask_bytes, 256));
+    int* counts = reinterpret_cast<int*>(base + cnt_off);
+    int* lists = static_cast<int*>(ctx->list_buf);
     // generation-stamped non-finite flag: no per-launch memset needed
     if (++ctx->gen == 0) {
         HIP_TRY(hipMemsetAsync(ctx->flag, 0, sizeof(unsigned), stream));
@@ -951,21 +917,24 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
 
     if (n_prims > 0) {
         prep_kernel<<<dim3((n_prims + kPrepThreads - 1) / kPrepThreads), dim3(kPrepThreads), 0,
-                      stream>>>(sd, dir, width, row_begin, row_end, tri, sph, boxes, clsv,
-                                colours, ctx->flag, ctx->gen, masks, n_words, n_cx);
+                      stream>>>(
+            sd, dir, width, row_begin, row_end, tri, sph, boxes, clsv, colours, ctx->flag,
+            ctx->gen);
         HIP_TRY(hipGetLastError());
     }
-    if (pe) {
-        HIP_TRY(hipEventRecord(pe[1], stream));
-        HIP_TRY(hipEventRecord(pe[2], stream));
-    }
+    if (pe) HIP_TRY(hipEventRecord(pe[1], stream));
+    coarse_kernel<<<dim3((n_coarse + 3) / 4), dim3(kThreads), 0, stream>>>(
+        boxes, n_prims, n_cx, n_coarse, row_begin, cap, counts, lists);
+    HIP_TRY(hipGetLastError());
+    if (pe) HIP_TRY(hipEventRecord(pe[2], stream));
     auto kern = ctx->trace_mode == 1 ? trace_kernel<1>
               : ctx->trace_mode == 2 ? trace_kernel<2>
               : ctx->trace_mode == 3 ? trace_kernel<3>
               : ctx->trace_mode == 4 ? trace_kernel<4> : trace_kernel<0>;
     kern<<<dim3((unsigned)n_bins), dim3(kThreads), 0, stream>>>(
-        sd, tri, sph, boxes, clsv, colours, masks, n_words, done, ctx->flag, ctx->gen, dir, width,
-        row_begin, row_end, n_bins_x, n_cx, fmt, out);
+        sd, tri, sph, boxes, clsv, colours, counts, lists, cap, ctx->flag, ctx->gen, dir, width,
+        row_begin,
+        row_end, n_bins_x, n_cx, fmt, out);
     HIP_TRY(hipGetLastError());
     if (pe) HIP_TRY(hipEventRecord(pe[3], stream));
     return RT_OK;
@@ -1019,7 +988,7 @@ void rt_destroy(rt_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-    for (void* p : {ctx->scene_buf, ctx->origin_buf, ctx->out_buf, ctx->rec_buf, ctx->mask_buf,
+    for (void* p : {ctx->scene_buf, ctx->origin_buf, ctx->out_buf, ctx->rec_buf, ctx->list_buf,
                     static_cast<void*>(ctx->flag)})
         if (p) (void)hipFree(p);
     for (auto& e : ctx->ev)
