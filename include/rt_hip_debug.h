@@ -1,0 +1,48 @@
+/*
+ * rt_hip_debug.h -- test and diagnostics hooks exported by librt_hip.so.
+ *
+ * Not part of the drop-in boundary (rt_hip.h) and with no reference
+ * counterpart: these let the test suite check the binned path's culling
+ * bounds on the host, check the device's fp32 rounding, and time ablated
+ * variants of the trace kernel.  A MainState integration never calls them.
+ */
+#ifndef RT_HIP_DEBUG_H
+#define RT_HIP_DEBUG_H
+
+#include <stdint.h>
+
+#include "rt_hip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Device sqrtf and x / 180.0f for n inputs (both must be correctly rounded
+ * for parity with the reference's SSE build, MainState.cpp:321, :400). */
+int rt_selftest_fp32(rt_ctx* ctx, const float* host_in, int32_t n,
+                     float* host_sqrt, float* host_div);
+
+/* Host evaluation of the prep kernel's per-triangle / per-sphere culling
+ * data (the same __host__ __device__ code): inclusive pixel box
+ * (x0, y0, x1, y1) and the 8-float tile classifier.  Return 1 when the
+ * primitive can report a hit at all (triangle) / has finite data (sphere). */
+int rt_debug_triangle_box(const float v0[3], const float v1[3],
+                          const float v2[3], const float dir[4], int32_t width,
+                          int32_t row_begin, int32_t row_end,
+                          int32_t box_out[4], float cls_out[8]);
+int rt_debug_sphere_box(const float origin[4], float radius,
+                        const float dir[4], int32_t width, int32_t row_begin,
+                        int32_t row_end, int32_t box_out[4], float cls_out[8]);
+
+/* Pixel shape of the tile one wave classifies and traces (w x h). */
+int rt_debug_tile_shape(int32_t* w, int32_t* h);
+
+/* Trace-kernel ablation for measurements: 0 = the real kernel, 1 = stores
+ * only, 2 = no per-pixel tests, 3 = no stores, 4 = tests without record
+ * loads.  Modes 1-4 produce wrong frames by design. */
+int rt_debug_set_trace_mode(rt_ctx* ctx, int mode);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RT_HIP_DEBUG_H */

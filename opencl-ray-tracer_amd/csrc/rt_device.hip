@@ -13,11 +13,11 @@
 //          which the exact test provably rejects.
 //   coarse one wave per 64x64 coarse bin: ordered compact candidate list
 //          (ballot + mbcnt), order = the reference's primitive order.
-//   trace  one 256-thread workgroup per 32x32 bin: the coarse list (ids +
-//          boxes) staged in LDS once per workgroup, one 16x16 tile per wave
-//          filtered by ballot, four pixels per lane, wave-uniform candidate
-//          walk on scalar record loads, exact per-lane tests, 16-B coalesced
-//          framebuffer stores.
+//   trace  one 256-thread workgroup per 16x64 bin: the coarse list (ids,
+//          boxes, tile classifiers) staged in LDS once per workgroup, one
+//          8x32 tile per wave filtered by ballot, four pixels per lane (rows
+//          8 apart), wave-uniform candidate walk on scalar record loads,
+//          exact per-lane tests, 16-B coalesced framebuffer stores.
 // Plus `generic`, a brute-force per-pixel kernel for arbitrary ray origins
 // and directions (the reference's kernel arguments 8-9 in full generality).
 //
@@ -33,6 +33,7 @@
 #include <vector>
 
 #include "rt_hip.h"
+#include "rt_hip_debug.h"
 
 #pragma clang fp contract(off)
 
@@ -60,6 +61,7 @@ constexpr int kBinH = 2 * kWaveTileH;
 constexpr int kCoarse = 64;       // coarse bin (candidate list) edge, pixels
 constexpr int kStage = 256;       // candidate entries staged in LDS per pass
 static_assert(64 % kBinW == 0 && 64 % kBinH == 0, "bins must tile a coarse bin");
+static_assert(kWaveTile <= 32 && kWaveTileH <= 32, "prep_triangle's margins assume <= 32 px tiles");
 constexpr int kThreads = 256;
 constexpr int kPrepThreads = 64;  // prep: one wave per block, spread over CUs
 constexpr double kEpsilon = 0.000001;      // MainState.cpp:15
@@ -93,7 +95,7 @@ static_assert(sizeof(SphRec) == 32, "SphRec layout");
 // Triangle: a = (v0x, v0y, au, bu), b = (av, bv, g, 0) with the exact
 // barycentrics u = au (x - v0x) + bu (y - v0y), v = av (x - v0x) + bv (y -
 // v0y) up to a margin g that also covers the fp64 rounding of the per-pixel
-// test, so a 16x16 tile can be proven fully outside (skip) or fully inside
+// test, so a wave tile can be proven fully outside (skip) or fully inside
 // (no u/v tests, t only) in fp32.  g = +inf disables both.
 // Sphere: a = (cx, cy, R2, 0): every pixel farther than sqrt(R2) misses.
 struct Cls {
@@ -185,8 +187,9 @@ __host__ __device__ inline bool prep_triangle(const float* a, const float* b, co
         const double err = (32.0 * eps + 4.0 * rho) * s + 32.0 * eps;
         const double g = 2.0 * err + 8.0 * eps * s + 32.0 * eps;
         // fp32 classifier planes and their margin.  The classifier only ever
-        // sees pixels of 16x16 tiles that overlap the box, so |x - v0x| and
-        // |y - v0y| are bounded by the padded box plus one tile: the margin
+        // sees pixels of wave tiles (at most 32 px on a side) that overlap the
+        // box, so |x - v0x| and |y - v0y| are bounded by the padded box plus
+        // 32 px: the margin
         // covers the fp64 test's rounding there (err_loc) and the fp32
         // rounding of the coefficients and of the plane evaluation (2^-24
         // each, x32 slack).
@@ -586,8 +589,8 @@ __device__ __forceinline__ void test_primitive(int p, int slot, bool inside, con
     return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), lane));
 }
 
-// Tile classification of one staged candidate against a 16x16 tile
-// [x0, x0+15] x [y0, y0+15] (fp32, conservative; see Cls).
+// Tile classification of one staged candidate against the wave tile
+// [x0, x0+kWaveTile-1] x [y0, y0+kWaveTileH-1] (fp32, conservative; see Cls).
 __device__ __forceinline__ void classify(const Cls& k, bool is_tri, float x0, float y0,
                                          bool* keep, bool* inside) {
     constexpr float kW = (float)(kWaveTile - 1), kH = (float)(kWaveTileH - 1);
@@ -1170,6 +1173,13 @@ int rt_debug_triangle_box(const float v0[3], const float v1[3], const float v2[3
 int rt_debug_set_trace_mode(rt_ctx* ctx, int mode) {
     if (!ctx || mode < 0 || mode > 4) return RT_ERR_INVALID_ARG;
     ctx->trace_mode = mode;
+    return RT_OK;
+}
+
+int rt_debug_tile_shape(int32_t* w, int32_t* h) {
+    if (!w || !h) return RT_ERR_INVALID_ARG;
+    *w = kWaveTile;
+    *h = kWaveTileH;
     return RT_OK;
 }
 

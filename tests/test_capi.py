@@ -9,10 +9,11 @@ import pytest
 
 REPO = Path(__file__).resolve().parents[1]
 HEADER = REPO / "include" / "rt_hip.h"
+DEBUG_HEADER = REPO / "include" / "rt_hip_debug.h"
 
 
-def declared_functions():
-    text = HEADER.read_text()
+def declared_functions(header=HEADER):
+    text = header.read_text()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     return sorted(set(re.findall(r"\b(rt_[a-z0-9_]+)\s*\(", text)))
 
@@ -29,6 +30,8 @@ def test_library_exports_every_declared_symbol(pkg):
     missing = [n for n in declared_functions() if not hasattr(lib, n)]
     assert not missing, missing
     assert set(declared_functions()) == set(pkg.EXPORTED_SYMBOLS)
+    hooks = declared_functions(DEBUG_HEADER)
+    assert hooks and not [n for n in hooks if not hasattr(lib, n)]
 
 
 def test_abi_version(pkg):

@@ -2,6 +2,8 @@
 scene packing vs the oracle, and the culling bounds of the prep kernel
 (same __host__ __device__ code) proven conservative against the oracle's
 per-pixel tests (MainState.cpp:257-327)."""
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -61,15 +63,23 @@ def test_pack_rgba8_matches_oracle(pkg, oracle):
 # ---------------------------------------------------------------------------
 # culling bounds
 # ---------------------------------------------------------------------------
-def classify_tile(cls, is_tri, x0, y0):
-    """numpy float32 mirror of the trace kernel's classify() (rt_device.hip)."""
+def tile_shape(pkg):
+    w, h = ctypes.c_int32(), ctypes.c_int32()
+    assert pkg.library().rt_debug_tile_shape(ctypes.byref(w), ctypes.byref(h)) == 0
+    return w.value, h.value
+
+
+def classify_tile(cls, is_tri, x0, y0, tw, th):
+    """numpy float32 mirror of the trace kernel's classify() (rt_device.hip)
+    on a tw x th wave tile."""
     f = np.float32
+    kw, kh = f(tw - 1), f(th - 1)
     a = cls[:4].astype(np.float32)
     b = cls[4:].astype(np.float32)
     x0, y0 = f(x0), f(y0)
     if is_tri:
-        xl, xh = x0 - a[0], (x0 + f(15)) - a[0]
-        yl, yh = y0 - a[1], (y0 + f(15)) - a[1]
+        xl, xh = x0 - a[0], (x0 + kw) - a[0]
+        yl, yh = y0 - a[1], (y0 + kh) - a[1]
         u1, u2, u3, u4 = a[2] * xl, a[2] * xh, a[3] * yl, a[3] * yh
         v1, v2, v3, v4 = b[0] * xl, b[0] * xh, b[1] * yl, b[1] * yh
         umin, umax = min(u1, u2) + min(u3, u4), max(u1, u2) + max(u3, u4)
@@ -80,8 +90,8 @@ def classify_tile(cls, is_tri, x0, y0):
         inside = (umin > g and umax < f(1) - g and vmin > g and vmax < f(1) - g
                   and umax + vmax < f(1) - g)
         return not out, bool(inside)
-    dx = max(max(x0 - a[0], a[0] - (x0 + f(15))), f(0))
-    dy = max(max(y0 - a[1], a[1] - (y0 + f(15))), f(0))
+    dx = max(max(x0 - a[0], a[0] - (x0 + kw)), f(0))
+    dy = max(max(y0 - a[1], a[1] - (y0 + kh)), f(0))
     return not (dx * dx + dy * dy > a[2]), False
 
 
@@ -129,6 +139,7 @@ def classify_pixels(cls, xs, ys):
 def test_triangle_box_and_tile_classifier_are_conservative(pkg, oracle, band):
     w, h = 176, 160
     rb, re = band
+    tw, th = tile_shape(pkg)
     rng = np.random.default_rng(7 + rb)
     n_inside_tiles = n_skip_tiles = 0
     for v in random_triangles(rng, w, h, 150):
@@ -142,20 +153,20 @@ def test_triangle_box_and_tile_classifier_are_conservative(pkg, oracle, band):
             assert box[0] <= xs.min() and xs.max() <= box[2]
             assert box[1] <= ys.min() + rb and ys.max() + rb <= box[3]
         # per-pixel pre-classification of every pixel inside the padded box
-        x0, x1 = max(box[0] - 16, 0), min(box[2] + 16, w - 1)
-        y0, y1 = max(box[1] - 16, rb), min(box[3] + 16, re - 1)
+        x0, x1 = max(box[0] - tw, 0), min(box[2] + tw, w - 1)
+        y0, y1 = max(box[1] - th, rb), min(box[3] + th, re - 1)
         if x0 <= x1 and y0 <= y1:
             ys, xs = np.mgrid[y0:y1 + 1, x0:x1 + 1]
             out_px, in_px = classify_pixels(cls, xs, ys)
             sub = hits[y0 - rb:y1 - rb + 1, x0:x1 + 1].astype(bool)
             assert not (out_px & sub).any(), v
             assert not (in_px & ~sub).any(), v
-        for ty in range(rb, re, 16):
-            for tx in range(0, w, 16):
-                if box[0] > tx + 15 or box[2] < tx or box[1] > ty + 15 or box[3] < ty:
+        for ty in range(rb, re, th):
+            for tx in range(0, w, tw):
+                if box[0] > tx + tw - 1 or box[2] < tx or box[1] > ty + th - 1 or box[3] < ty:
                     continue  # the kernel classifies only tiles the box touches
-                keep, inside = classify_tile(cls, True, tx, ty)
-                tile = hits[ty - rb:ty - rb + 16, tx:tx + 16]
+                keep, inside = classify_tile(cls, True, tx, ty, tw, th)
+                tile = hits[ty - rb:ty - rb + th, tx:tx + tw]
                 if not keep:
                     n_skip_tiles += 1
                     assert not tile.any(), (v, tx, ty)
@@ -167,6 +178,7 @@ def test_triangle_box_and_tile_classifier_are_conservative(pkg, oracle, band):
 
 def test_sphere_box_and_tile_classifier_are_conservative(pkg, oracle):
     w, h = 160, 128
+    tw, th = tile_shape(pkg)
     rng = np.random.default_rng(11)
     for i in range(120):
         c = np.float32([rng.uniform(-30, w + 30), rng.uniform(-30, h + 30),
@@ -181,8 +193,8 @@ def test_sphere_box_and_tile_classifier_are_conservative(pkg, oracle):
             assert box[1] <= ys.min() and ys.max() <= box[3]
         elif box[0] > box[2]:
             continue
-        for ty in range(0, h, 16):
-            for tx in range(0, w, 16):
-                keep, _ = classify_tile(cls, False, tx, ty)
+        for ty in range(0, h, th):
+            for tx in range(0, w, tw):
+                keep, _ = classify_tile(cls, False, tx, ty, tw, th)
                 if not keep:
-                    assert not hits[ty:ty + 16, tx:tx + 16].any(), (c, r, tx, ty)
+                    assert not hits[ty:ty + th, tx:tx + tw].any(), (c, r, tx, ty)
