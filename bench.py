@@ -133,8 +133,9 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         wall_ms = float(tt.item())
 
-    # Per-kernel durations: a second, profiled pass (HIP events on the launch
-    # stream between prep / bin / trace, inside librt_hip.so).
+    # Per-kernel durations: a second, profiled pass.  librt_hip.so attaches
+    # start/stop HIP events to each kernel's own dispatch packet on the launch
+    # stream (hipExtLaunchKernelGGL), so they time the kernel itself.
     rt.profile(True)
     for _ in range(args.steps):
         step()
@@ -211,7 +212,7 @@ def main():
                        "parallelism": f"row-bands x{world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic, "kernel": "trace_kernel",
+                         "traffic": traffic, "kernel": "trace3_kernel",
                          "kernel_ms": round(trace_ms, 4), "prep_ms": round(prep_ms, 4),
                          "bin_ms": round(bin_ms, 4), "algo_bytes_per_launch": algo_bytes},
             "event_ms_per_step": round(event_ms, 4),

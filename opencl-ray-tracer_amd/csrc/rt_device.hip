@@ -11,20 +11,22 @@
 //   prep   one lane per primitive: per-triangle fp64 constants, per-sphere
 //          fp32 constants, and a conservative integer pixel box outside of
 //          which the exact test provably rejects.
-//   coarse one wave per 64x64 coarse bin: ordered compact candidate list
-//          (ballot + mbcnt), order = the reference's primitive order.
-//   trace  one 256-thread workgroup per 16x64 bin: the coarse list (ids,
-//          boxes, tile classifiers) staged in LDS once per workgroup, one
-//          8x32 tile per wave filtered by ballot, four pixels per lane (rows
-//          8 apart), wave-uniform candidate walk on scalar record loads,
-//          exact per-lane tests, 16-B coalesced framebuffer stores.
+//   coarse one wave per 64x64 coarse bin: the ordered list of primitives
+//          whose box touches the bin (ballot + mbcnt, the reference's
+//          primitive order), each with a word of 2 bits per 8x32 wave tile
+//          of the bin (tile classifier: skip / test / u,v proven inside).
+//   trace  one wave per 8x32 tile, four pixels per lane (rows 8 apart):
+//          count, ids, tile words and records all on scalar loads, exact
+//          per-lane tests, 16-B coalesced framebuffer stores.
 // Plus `generic`, a brute-force per-pixel kernel for arbitrary ray origins
 // and directions (the reference's kernel arguments 8-9 in full generality).
 //
 // Build: -ffp-contract=off (and the pragma below): every operation rounds
 // once, as x86-64 SSE does in the reference's CPU build.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdint>
@@ -46,22 +48,26 @@ namespace {
 #ifndef RT_ROWS
 #define RT_ROWS 4                 // pixels per lane (rows, 64/RT_TILE_W apart)
 #endif
-#ifndef RT_TILECLS
-#define RT_TILECLS 1              // per-tile plane classification of candidates
+#ifndef RT_TRACE_WAVES
+#define RT_TRACE_WAVES 8          // amdgpu_waves_per_eu floor for trace (0 = none)
 #endif
-#ifndef RT_PIXCLS
-#define RT_PIXCLS 0               // per-pixel fp32 pre-classification
+#ifndef RT_NT_STORE
+#define RT_NT_STORE 0             // nontemporal frame stores
+#endif
+#ifndef RT_TIMELINE
+#define RT_TIMELINE 0             // diagnostics: per-wave phase timestamps
 #endif
 constexpr int kWaveTile = RT_TILE_W;                       // wave tile width
 constexpr int kRowsPerLane = RT_ROWS;
 constexpr int kLaneRows = 64 / RT_TILE_W;                  // lane rows per pass
 constexpr int kWaveTileH = kLaneRows * RT_ROWS;            // wave tile height
-constexpr int kBinW = 2 * kWaveTile;  // bin = workgroup tile (2x2 wave tiles)
-constexpr int kBinH = 2 * kWaveTileH;
 constexpr int kCoarse = 64;       // coarse bin (candidate list) edge, pixels
-constexpr int kStage = 256;       // candidate entries staged in LDS per pass
-static_assert(64 % kBinW == 0 && 64 % kBinH == 0, "bins must tile a coarse bin");
-static_assert(kWaveTile <= 32 && kWaveTileH <= 32, "prep_triangle's margins assume <= 32 px tiles");
+static_assert(kCoarse % kWaveTile == 0 && kCoarse % kWaveTileH == 0,
+              "wave tiles must tile a coarse bin");
+// prep_triangle's classifier margin covers tiles that overhang a box by up to
+// kTileSpan pixels on any side
+constexpr int kTileSpan = kWaveTile > kWaveTileH ? kWaveTile : kWaveTileH;
+static_assert(kTileSpan <= 64, "tile span");
 constexpr int kThreads = 256;
 constexpr int kPrepThreads = 64;  // prep: one wave per block, spread over CUs
 constexpr double kEpsilon = 0.000001;      // MainState.cpp:15
@@ -187,15 +193,16 @@ __host__ __device__ inline bool prep_triangle(const float* a, const float* b, co
         const double err = (32.0 * eps + 4.0 * rho) * s + 32.0 * eps;
         const double g = 2.0 * err + 8.0 * eps * s + 32.0 * eps;
         // fp32 classifier planes and their margin.  The classifier only ever
-        // sees pixels of wave tiles (at most 32 px on a side) that overlap the
-        // box, so |x - v0x| and |y - v0y| are bounded by the padded box plus
-        // 32 px: the margin
+        // sees pixels of wave tiles (at most kTileSpan px on a side) that
+        // overlap the box, so |x - v0x| and |y - v0y| are bounded by the padded
+        // box plus kTileSpan: the margin
         // covers the fp64 test's rounding there (err_loc) and the fp32
         // rounding of the coefficients and of the plane evaluation (2^-24
         // each, x32 slack).
         const double padx0 = 8.0 * (mxx - mnx) * g + 0.5, pady0 = 8.0 * (mxy - mny) * g + 0.5;
-        const double tx_loc = fmax(fabs(mnx - padx0 - 32.0 - v0[0]), fabs(mxx + padx0 + 32.0 - v0[0])) + 1.0;
-        const double ty_loc = fmax(fabs(mny - pady0 - 32.0 - v0[1]), fabs(mxy + pady0 + 32.0 - v0[1])) + 1.0;
+        const double span = (double)kTileSpan;
+        const double tx_loc = fmax(fabs(mnx - padx0 - span - v0[0]), fabs(mxx + padx0 + span - v0[0])) + 1.0;
+        const double ty_loc = fmax(fabs(mny - pady0 - span - v0[1]), fabs(mxy + pady0 + span - v0[1])) + 1.0;
         const double s_loc = (tx_loc * (fabs(p0) + fabs(e1[1] * dz)) +
                               ty_loc * (fabs(p1) + fabs(e1[0] * dz))) * fabs(inv_det);
         const double err_loc = (32.0 * eps + 4.0 * rho) * s_loc + 32.0 * eps;
@@ -453,119 +460,57 @@ __global__ void __launch_bounds__(kPrepThreads) prep_kernel(
     if (bad) atomicMax(nonfinite_flag, gen);
 }
 
-// Coarse binning: one wave per 64x64-pixel coarse bin writes the ordered
-// list of primitives whose box touches it (ballot + mbcnt compaction keeps
-// the reference's primitive order: cubes' triangles, then spheres).
-__global__ void __launch_bounds__(kThreads) coarse_kernel(
-    const int4* __restrict__ boxes, int n_prims, int n_cx, int n_coarse, int row_begin,
-    int cap, int* __restrict__ counts, int* __restrict__ lists) {
-    const int cb = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
-    if (cb >= n_coarse) return;  // wave-uniform
-    const int lane = threadIdx.x & 63;
-    const int x0 = (cb % n_cx) * kCoarse, x1 = x0 + kCoarse - 1;
-    const int y0 = row_begin + (cb / n_cx) * kCoarse, y1 = y0 + kCoarse - 1;
-    int* out = lists + (int64_t)cb * cap;
-    int count = 0;
-    // boxes are loaded kBatch chunks at a time so the loads overlap (the
-    // loop is otherwise a chain of dependent L2 round trips)
-    constexpr int kBatch = 8;
-    for (int base = 0; base < n_prims; base += 64 * kBatch) {
-        int4 bb[kBatch];
-#pragma unroll
-        for (int k = 0; k < kBatch; ++k) {
-            const int p = base + 64 * k + lane;
-            bb[k] = p < n_prims ? boxes[p] : make_int4(1 << 30, 1 << 30, -(1 << 30), -(1 << 30));
-        }
-#pragma unroll
-        for (int k = 0; k < kBatch; ++k) {
-            const int4 b = bb[k];
-            const bool ov = b.x <= x1 && b.z >= x0 && b.y <= y1 && b.w >= y0;
-            const unsigned long long m = __ballot(ov);
-            if (ov) {
-                const unsigned below = __builtin_amdgcn_mbcnt_hi(
-                    (unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-                out[count + (int)below] = base + 64 * k + lane;
-            }
-            count += __popcll(m);
-        }
-    }
-    if (lane == 0) counts[cb] = count;
-}
+
+#if RT_TIMELINE
+// per wave: realtime at entry / first staged / walked / stores issued,
+// s_memtime at entry / end, HW_ID, XCC_ID
+__device__ unsigned* g_timeline;
+__device__ __forceinline__ unsigned rt_now() { return (unsigned)__builtin_amdgcn_s_memrealtime(); }
+#define TL_MARK(v) const unsigned v = rt_now()
+#else
+#define TL_MARK(v)
+#endif
 
 // Per-lane exact tests of one candidate primitive `p` (wave-uniform) on the
 // lane's kRowsPerLane pixels.  Triangles: MainState.cpp:257-298 restated on
 // the per-triangle constants (see TriRec); `inside` (wave-uniform) means the
 // tile classifier proved every pixel of the tile passes the u/v tests, so
 // only the exact t is computed.  Spheres: :300-327 on SphRec.
-__device__ __forceinline__ void test_primitive(int p, int slot, bool inside, const Cls& k,
-                                               int n_tri, const TriRec* __restrict__ tri,
-                                               const SphRec* __restrict__ sph, double px,
-                                               float pxf, const double* py, const float* pyf,
-                                               float* closest, int* hit) {
-    if (p < n_tri) {
-        const TriRec r = tri[p];
+// Select-based form: every row evaluates the whole test and a compare picks
+// the result, so the wave never diverges inside the walk.  The per-lane
+// (row-invariant) products are hoisted; each is the same fp64 operation on
+// the same operands as in MainState.cpp:257-298, so values are unchanged.
+__device__ __forceinline__ void test_tri(const TriRec& r, int slot, bool inside, double px,
+                                         const double* py, float* closest, int* hit) {
+    {
         const double tx = px - r.v0x;
-        if (inside) {
-#pragma unroll
-            for (int j = 0; j < kRowsPerLane; ++j) {
-                const double ty = py[j] - r.v0y;
-                const double q2 = tx * r.e1y - ty * r.e1x;
-                const double q0 = ty * r.e1z - r.k0;
-                const double q1 = r.k1 - tx * r.e1z;
-                const double t = (r.e2x * q0 + r.e2y * q1 + r.e2z * q2) * r.inv_det;
-                const float tf = (float)t;
-                if (tf < closest[j]) {
-                    closest[j] = tf;
-                    hit[j] = slot;
-                }
-            }
-            return;
-        }
-        // Partial tile: classify each pixel on the fp32 planes first (same
-        // margin as the tile classifier); only pixels inside the margin band
-        // of an edge run the full fp64 u/v test, proven-inside pixels compute
-        // t only, proven-outside pixels are done.
-#if RT_PIXCLS
-        const float xl = pxf - k.a.x;
-        const float ux = k.a.z * xl, vx = k.b.x * xl;
-        const float g = k.b.z;
-#endif
+        const double txe1y = tx * r.e1y;               // q2 = tx*e1y - ty*e1x
+        const double q1 = r.k1 - tx * r.e1z;           // q1 = tz*e1x - tx*e1z
+        const double e2yq1 = r.e2y * q1;
+        const double txp0 = tx * r.p0;                 // u = (tx*p0 + ty*p1) * inv_det
 #pragma unroll
         for (int j = 0; j < kRowsPerLane; ++j) {
-#if RT_PIXCLS
-            const float yl = pyf[j] - k.a.y;
-            const float ul = ux + k.a.w * yl;
-            const float vl = vx + k.b.y * yl;
-            const float wl = ul + vl;
-            const bool out = ul < -g || ul > 1.0f + g || vl < -g || vl > 1.0f + g || wl > 1.0f + g;
-            const bool in = ul > g && ul < 1.0f - g && vl > g && vl < 1.0f - g && wl < 1.0f - g;
-            if (out) continue;
-#else
-            const bool in = false;
-#endif
             const double ty = py[j] - r.v0y;
-            const double q2 = tx * r.e1y - ty * r.e1x;
-            bool pass = in;
-            if (!in) {
-                // u = ((tx*p0 + ty*p1) + tz*p2) * inv_det, tz*p2 == +-0 for d = (0,0,D)
-                const double u = (tx * r.p0 + ty * r.p1) * r.inv_det;
-                // v = ((d0*q0 + d1*q1) + d2*q2) * inv_det, d0 = d1 = +-0
+            const double q2 = txe1y - ty * r.e1x;
+            const double q0 = ty * r.e1z - r.k0;
+            const double t = ((r.e2x * q0 + e2yq1) + r.e2z * q2) * r.inv_det;
+            const float tf = (float)t;
+            bool pass = true;
+            if (!inside) {  // wave-uniform
+                const double u = (txp0 + ty * r.p1) * r.inv_det;
                 const double v = (r.dz * q2) * r.inv_det;
-                pass = !(u < 0.0 || u > 1.0) && !(v < 0.0 || u + v > 1.0);
+                pass = !((u < 0.0) | (u > 1.0) | (v < 0.0) | (u + v > 1.0));
             }
-            if (pass) {
-                const double q0 = ty * r.e1z - r.k0;
-                const double q1 = r.k1 - tx * r.e1z;
-                const double t = (r.e2x * q0 + r.e2y * q1 + r.e2z * q2) * r.inv_det;
-                const float tf = (float)t;
-                if (tf < closest[j]) {
-                    closest[j] = tf;
-                    hit[j] = slot;
-                }
-            }
+            const bool take = pass & (tf < closest[j]);
+            closest[j] = take ? tf : closest[j];
+            hit[j] = take ? slot : hit[j];
         }
-    } else {
-        const SphRec s = sph[p - n_tri];
+    }
+}
+
+__device__ __forceinline__ void test_sph(const SphRec& s, int slot, float pxf, const float* pyf,
+                                         float* closest, int* hit) {
+    {
         const float lx = s.cx - pxf;
         const float lx2 = lx * lx;
 #pragma unroll
@@ -573,20 +518,13 @@ __device__ __forceinline__ void test_primitive(int p, int slot, bool inside, con
             const float ly = s.cy - pyf[j];
             const float a = lx2 + ly * ly;
             const float dist2 = (a + s.kzw) - s.tca2;
-            if (!(dist2 > s.r2)) {
-                const float thc = sqrtf(s.r2 - dist2);
-                const float t0 = s.tca - thc;
-                if (t0 != 0.0f && t0 < closest[j]) {
-                    closest[j] = t0;
-                    hit[j] = slot;
-                }
-            }
+            const float thc = sqrtf(s.r2 - dist2);
+            const float t0 = s.tca - thc;
+            const bool take = !(dist2 > s.r2) & (t0 != 0.0f) & (t0 < closest[j]);
+            closest[j] = take ? t0 : closest[j];
+            hit[j] = take ? slot : hit[j];
         }
     }
-}
-
-[[maybe_unused]] __device__ __forceinline__ float readlane_f(float v, int lane) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), lane));
 }
 
 // Tile classification of one staged candidate against the wave tile
@@ -617,49 +555,201 @@ __device__ __forceinline__ void classify(const Cls& k, bool is_tri, float x0, fl
 
 __device__ __forceinline__ void store_pixel(void* __restrict__ out, int out_format, int64_t idx,
                                             int4v pix) {
+#if RT_NT_STORE
+    // streaming stores: the frame is written once and never re-read here
+    if (out_format == RT_FORMAT_I32X4)
+        __builtin_nontemporal_store(pix, reinterpret_cast<int4v*>(out) + idx);
+    else
+        __builtin_nontemporal_store(pack_rgba8(pix), reinterpret_cast<unsigned*>(out) + idx);
+#else
     if (out_format == RT_FORMAT_I32X4)
         reinterpret_cast<int4v*>(out)[idx] = pix;
     else
         reinterpret_cast<unsigned*>(out)[idx] = pack_rgba8(pix);
+#endif
 }
 
-// One workgroup per bin (2x2 wave tiles), kRowsPerLane pixels per lane.
-// The parent coarse bin's candidate list (ids, boxes, classifiers) is staged
-// in LDS once per workgroup; each wave filters it against its own tile (one
-// ballot per 64 entries, compacted in order into a per-wave LDS list with the
-// tile classification in bit 31), then walks that list with one flat uniform
-// loop: scalar record loads -> per-lane exact tests.
-// kMode is a diagnostics ablation (rt_debug_set_trace_mode): 0 = the real
-// kernel, 1 = stores only (the store floor of this exact pattern), 2 = stage
-// and filter candidates but skip the per-pixel tests, 3 = everything but the
-// framebuffer stores, 4 = per-pixel tests without the per-candidate record
-// loads (wrong pixels; timing only).
+// Shade (MainState.cpp:396-407) and store one lane's kRowsPerLane pixels.
 template <int kMode>
-__global__ void __launch_bounds__(kThreads) trace_kernel(
+__device__ __forceinline__ void shade_store(const float4* __restrict__ colours,
+                                            const float* closest, const int* hit, int x, int y0,
+                                            int width, int row_begin, int row_end,
+                                            int out_format, void* __restrict__ out) {
+    bool lane_hit = false;
+#pragma unroll
+    for (int j = 0; j < kRowsPerLane; ++j) lane_hit |= hit[j] >= 0;
+    const bool any_hit = __ballot(lane_hit) != 0ull;
+    int4v pix[kRowsPerLane];
+#pragma unroll
+    for (int j = 0; j < kRowsPerLane; ++j) pix[j] = int4v{0, 0, 0, 255};
+    if (any_hit) {
+        float4 col[kRowsPerLane];
+#pragma unroll
+        for (int j = 0; j < kRowsPerLane; ++j) col[j] = colours[hit[j] >= 0 ? hit[j] : 0];
+#pragma unroll
+        for (int j = 0; j < kRowsPerLane; ++j) {
+            const int4v c = shade_hit(hit[j] >= 0 ? closest[j] : 0.0f, col[j]);
+            if (hit[j] >= 0) pix[j] = c;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < kRowsPerLane; ++j) {
+        const int y = y0 + kLaneRows * j;
+        const bool store = kMode != 3 || pix[j].x == 0x7fffffff;
+        if (x < width && y < row_end && store)
+            store_pixel(out, out_format, (int64_t)(y - row_begin) * width + x, pix[j]);
+    }
+}
+
+
+
+// Tiles of one coarse bin: kCoarse / kWaveTile x kCoarse / kWaveTileH.
+constexpr int kTilesX = kCoarse / kWaveTile;
+constexpr int kTilesY = kCoarse / kWaveTileH;
+static_assert(kTilesX * kTilesY <= 16, "two bits per tile in one 32-bit word");
+
+// Coarse binning with per-tile classification: one wave per coarse bin.
+// (1) the ids whose box touches the coarse bin are compacted, in primitive
+// order, into LDS (rounds of kRound); (2) the (candidate, tile) pairs are
+// spread over the lanes, 16 lanes per candidate, each testing box overlap +
+// tile classifier and OR-ing its two bits (bit 2t keep, bit 2t+1 inside)
+// into the candidate's LDS word; (3) candidates kept by some tile are
+// appended in order.  Output: counts[cb]; ids at lists[cb * 2 * half_cap
+// ...] and tile words at lists[cb * 2 * half_cap + half_cap ...].
+#ifndef RT_C3_ROUND
+#define RT_C3_ROUND 64
+#endif
+#ifndef RT_C3_BATCH
+#define RT_C3_BATCH 8
+#endif
+constexpr int kRound = RT_C3_ROUND;
+__global__ void __launch_bounds__(64) coarse3_kernel(
+    const int4* __restrict__ boxes, const Cls* __restrict__ cls, int n_prims, int n_tri,
+    int n_cx, int n_coarse, int row_begin, int half_cap, int* __restrict__ counts,
+    int* __restrict__ lists) {
+    __shared__ int s_ids[kRound];
+    __shared__ unsigned s_tm[kRound];
+    __shared__ int4 s_box[kRound];
+    __shared__ Cls s_cls[kRound];
+    const int cb = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int x0 = (cb % n_cx) * kCoarse, x1 = x0 + kCoarse - 1;
+    const int y0 = row_begin + (cb / n_cx) * kCoarse, y1 = y0 + kCoarse - 1;
+    int* out_id = lists + (int64_t)cb * 2 * half_cap;
+    int* out_tm = out_id + half_cap;
+    int count = 0;   // appended to the output
+    int staged = 0;  // ids in s_ids
+    constexpr int kBatch = RT_C3_BATCH;
+    auto classify_round = [&](int n) {
+        __builtin_amdgcn_wave_barrier();
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        // each candidate's box and classifier into LDS once
+        for (int e = lane; e < n; e += 64) {
+            const int id = s_ids[e];
+            s_tm[e] = 0u;
+            s_box[e] = boxes[id];
+            s_cls[e] = cls[id];
+        }
+        __builtin_amdgcn_wave_barrier();
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        constexpr int kTiles = kTilesX * kTilesY;
+        for (int q0 = 0; q0 < n * kTiles; q0 += 64) {
+            const int q = q0 + lane;
+            if (q < n * kTiles) {
+                const int c = q / kTiles, t = q % kTiles;
+                const int id = s_ids[c];
+                const int4 pb = s_box[c];
+                const int tx = x0 + (t % kTilesX) * kWaveTile;
+                const int ty = y0 + (t / kTilesX) * kWaveTileH;
+                bool keep = false, inside = false;
+                if (pb.x <= tx + kWaveTile - 1 && pb.z >= tx && pb.y <= ty + kWaveTileH - 1 &&
+                    pb.w >= ty)
+                    classify(s_cls[c], id < n_tri, (float)tx, (float)ty, &keep, &inside);
+                const unsigned bits = (keep ? 1u : 0u) | (keep && inside ? 2u : 0u);
+                if (bits) atomicOr(&s_tm[c], bits << (2 * t));
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        for (int e0 = 0; e0 < n; e0 += 64) {
+            const int e = e0 + lane;
+            const unsigned tm = e < n ? s_tm[e] : 0u;
+            const bool any = tm != 0u;
+            const unsigned long long m2 = __ballot(any);
+            if (any) {
+                const unsigned below = __builtin_amdgcn_mbcnt_hi(
+                    (unsigned)(m2 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m2, 0u));
+                out_id[count + (int)below] = s_ids[e];
+                out_tm[count + (int)below] = (int)tm;
+            }
+            count += __popcll(m2);
+        }
+        __builtin_amdgcn_wave_barrier();
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    };
+    for (int base = 0; base < n_prims; base += 64 * kBatch) {
+        int4 bb[kBatch];
+#pragma unroll
+        for (int k = 0; k < kBatch; ++k) {
+            const int p = base + 64 * k + lane;
+            bb[k] = p < n_prims ? boxes[p] : make_int4(1 << 30, 1 << 30, -(1 << 30), -(1 << 30));
+        }
+#pragma unroll
+        for (int k = 0; k < kBatch; ++k) {
+            const int4 b = bb[k];
+            const bool ov = b.x <= x1 && b.z >= x0 && b.y <= y1 && b.w >= y0;
+            const unsigned long long m = __ballot(ov);
+            const int n_ov = __popcll(m);
+            if (n_ov == 0) continue;
+            if (staged + n_ov > kRound) {
+                classify_round(staged);
+                staged = 0;
+            }
+            if (ov) {
+                const unsigned below = __builtin_amdgcn_mbcnt_hi(
+                    (unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+                s_ids[staged + (int)below] = base + 64 * k + lane;
+            }
+            staged += n_ov;
+        }
+    }
+    if (staged) classify_round(staged);
+    if (lane == 0) counts[cb] = count;
+}
+
+#if RT_TRACE_WAVES > 0
+#define RT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(RT_TRACE_WAVES)))
+#else
+#define RT_TRACE_ATTR
+#endif
+
+// One wave per kWaveTile x kWaveTileH tile, all candidate data on scalar
+// loads: count, then ids and tile words 8 at a time, then the records of
+// the candidates this tile keeps (in the reference's primitive order).
+template <int kMode>
+__global__ void __launch_bounds__(64) RT_TRACE_ATTR trace3_kernel(
     SceneDev scene, const TriRec* __restrict__ tri, const SphRec* __restrict__ sph,
-    const int4* __restrict__ boxes, const Cls* __restrict__ cls,
     const float4* __restrict__ colours, const int* __restrict__ counts,
-    const int* __restrict__ lists, int cap, const unsigned* __restrict__ nonfinite_flag,
-    unsigned gen, float4 dir, int width, int row_begin, int row_end, int n_bins_x, int n_cx,
+    const int* __restrict__ lists, int half_cap, const unsigned* __restrict__ nonfinite_flag,
+    unsigned gen, float4 dir, int width, int row_begin, int row_end, int n_tiles_x, int n_cx,
     int out_format, void* __restrict__ out) {
-    __shared__ int s_id[kStage];
-    __shared__ int4 s_box[kStage];
-    __shared__ Cls s_cls[kStage];
-    __shared__ int s_wlist[kThreads / 64][kStage];
-    const int bin = blockIdx.x;
-    const int wave = threadIdx.x >> 6;
-    const int lane = threadIdx.x & 63;
-    const int bin_x = (bin % n_bins_x) * kBinW;
-    const int bin_y = (bin / n_bins_x) * kBinH;  // relative to row_begin
-    const int tile_x = bin_x + (wave & 1) * kWaveTile;
-    const int tile_y = row_begin + bin_y + (wave >> 1) * kWaveTileH;
+    const int tile = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int rel_x = (tile % n_tiles_x) * kWaveTile;
+    const int rel_y = (tile / n_tiles_x) * kWaveTileH;  // relative to row_begin
+    const int tile_x = rel_x, tile_y = row_begin + rel_y;
     const int x = tile_x + (lane % kWaveTile);
     const int y0 = tile_y + (lane / kWaveTile);
     const int n_tri = 12 * scene.n_cubes;
+    const int cb = (rel_y / kCoarse) * n_cx + rel_x / kCoarse;
+    const int t = ((rel_y % kCoarse) / kWaveTileH) * kTilesX + (rel_x % kCoarse) / kWaveTile;
+    TL_MARK(tl0);
+#if RT_TIMELINE
+    const unsigned long long tlc0 = __builtin_amdgcn_s_memtime();
+#endif
 
     if (kMode == 0 && *nonfinite_flag == gen) {
-        // Non-finite scene data: the algebraic shortcuts of the binned path
-        // assume finite values, so run the reference algorithm verbatim.
+        // Non-finite scene data: run the reference algorithm verbatim.
 #pragma unroll 1
         for (int j = 0; j < kRowsPerLane; ++j) {
             const int y = y0 + kLaneRows * j;
@@ -672,7 +762,7 @@ __global__ void __launch_bounds__(kThreads) trace_kernel(
     }
 
     float closest[kRowsPerLane];
-    int hit[kRowsPerLane];  // colour slot of the closest primitive, -1 = none
+    int hit[kRowsPerLane];
     double py[kRowsPerLane];
     float pyf[kRowsPerLane];
 #pragma unroll
@@ -684,81 +774,54 @@ __global__ void __launch_bounds__(kThreads) trace_kernel(
     }
     const double px = (double)x;
     const float pxf = (float)x;
-    const int tx1 = tile_x + kWaveTile - 1, ty1 = tile_y + kWaveTileH - 1;
 
-    const int cb = (bin_y / kCoarse) * n_cx + bin_x / kCoarse;
     const int count = kMode == 1 ? 0 : counts[cb];
-    const int* __restrict__ list = lists + (int64_t)cb * cap;
-    int* wlist = s_wlist[wave];
-    for (int s0 = 0; s0 < count; s0 += kStage) {
-        const int n = min(kStage, count - s0);
-        if (s0 > 0) __syncthreads();  // previous stage fully consumed
-        for (int i = threadIdx.x; i < n; i += kThreads) {
-            const int id = list[s0 + i];
-            s_id[i] = id;
-            s_box[i] = boxes[id];
-            s_cls[i] = cls[id];
+    const int* __restrict__ ids = lists + (int64_t)cb * 2 * half_cap;
+    const int* __restrict__ tms = ids + half_cap;
+    TL_MARK(tl1);
+    for (int i0 = 0; i0 < count; i0 += 8) {
+        int idv[8], tmv[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            idv[k] = ids[i0 + k];  // half_cap is a multiple of 8 past the count
+            tmv[k] = tms[i0 + k];
         }
-        __syncthreads();
-        // filter: this wave's candidates, in order, into wlist
-        int wn = 0;
-        for (int c = 0; c < n; c += 64) {
-            const int e = c + lane;
-            bool keep = false, inside = false;
-            int id = 0;
-            if (e < n) {
-                const int4 b = s_box[e];
-                id = s_id[e];
-                if (b.x <= tx1 && b.z >= tile_x && b.y <= ty1 && b.w >= tile_y) {
-#if RT_TILECLS
-                    classify(s_cls[e], id < n_tri, (float)tile_x, (float)tile_y, &keep, &inside);
-#else
-                    keep = true;
-#endif
-                }
-            }
-            const unsigned long long m = __ballot(keep);
-            if (keep) {
-                const unsigned below = __builtin_amdgcn_mbcnt_hi(
-                    (unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-                wlist[wn + (int)below] = id | (inside ? (int)0x80000000u : 0);
-            }
-            wn += __popcll(m);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        for (int i = 0; i < wn; ++i) {
-            const int v = __builtin_amdgcn_readfirstlane(wlist[i]);
-            const int p = v & 0x7fffffff;
+        const int n = min(8, count - i0);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if (k >= n) break;
+            const unsigned bits = ((unsigned)tmv[k] >> (2 * t)) & 3u;
+            if (!(bits & 1u)) continue;
+            const int p = idv[k];
             if (kMode == 2) {
-                hit[0] = hit[0] > p ? hit[0] : -1;  // keep the walk alive
+                hit[0] = hit[0] > p ? hit[0] : -1;
                 continue;
             }
-            const int slot = p < n_tri ? p / 12 : scene.n_cubes + (p - n_tri);
-            // kMode 4: same tests on record 0 / sphere 0 (no dependent record loads)
-            const int pr = kMode == 4 ? (p < n_tri ? 0 : n_tri) : p;
-            test_primitive(pr, slot, v < 0, Cls{}, n_tri, tri, sph, px, pxf, py, pyf, closest,
-                           hit);
+            if (p < n_tri) {
+                const TriRec r = tri[p];
+                asm volatile("" ::"s"(r.p0), "s"(r.p1), "s"(r.dz));
+                test_tri(r, p / 12, (bits & 2u) != 0u, px, py, closest, hit);
+            } else {
+                const SphRec r = sph[p - n_tri];
+                test_sph(r, scene.n_cubes + (p - n_tri), pxf, pyf, closest, hit);
+            }
         }
     }
-
-    // Shade + store.  A wave whose pixels all missed (ballot) stores the
-    // black pattern without touching the colour table.
-    bool lane_hit = false;
-#pragma unroll
-    for (int j = 0; j < kRowsPerLane; ++j) lane_hit |= hit[j] >= 0;
-    const bool any_hit = __ballot(lane_hit) != 0ull;
-#pragma unroll
-    for (int j = 0; j < kRowsPerLane; ++j) {
-        const int y = y0 + kLaneRows * j;
-        int4v pix{0, 0, 0, 255};
-        if (any_hit && hit[j] >= 0) pix = shade_hit(closest[j], colours[hit[j]]);
-        // kMode 3: everything but the stores (a store the compiler cannot drop)
-        const bool store = kMode != 3 || pix.x == 0x7fffffff;
-        if (x < width && y < row_end && store)
-            store_pixel(out, out_format, (int64_t)(y - row_begin) * width + x, pix);
+    TL_MARK(tl2);
+    shade_store<kMode>(colours, closest, hit, x, y0, width, row_begin, row_end, out_format, out);
+#if RT_TIMELINE
+    {
+        const unsigned tl3 = rt_now();
+        const unsigned long long tlc3 = __builtin_amdgcn_s_memtime();
+        if (lane == 0) {
+            unsigned* o = g_timeline + 8 * (int64_t)tile;
+            o[0] = tl0; o[1] = tl1; o[2] = tl2; o[3] = tl3;
+            o[4] = (unsigned)tlc0; o[5] = (unsigned)tlc3;
+            o[6] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+            o[7] = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+        }
     }
+#endif
 }
 
 // fp32 self-test: the device's sqrtf and '/' must be correctly rounded.
@@ -785,11 +848,12 @@ struct rt_ctx {
     void* list_buf = nullptr;   size_t list_cap = 0;    // coarse-bin candidate lists
     unsigned* flag = nullptr;   // non-finite scene flag (generation-stamped)
     unsigned gen = 0;
-    int trace_mode = 0;  // diagnostics ablation, see trace_kernel
+    int trace_mode = 0;  // diagnostics ablation, see trace3_kernel
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-    // profiling
+    // profiling: per render, start/stop events of the prep, coarse and trace
+    // kernels, attached to the kernels' own dispatch packets
     bool profile = false;
-    std::vector<hipEvent_t> prof_events;  // quads: start, prep, coarse, trace
+    std::vector<hipEvent_t> prof_events;
     int32_t prof_count = 0;
 };
 
@@ -838,6 +902,27 @@ int check_args(const rt_scene* s, int32_t width, int32_t height, int32_t row_beg
         if ((x) != hipSuccess) return RT_ERR_HIP;     \
     } while (0)
 
+// Launch `kernel` on `stream`; with profiling events, through
+// hipExtLaunchKernelGGL so the start/stop timestamps are the kernel's own
+// (no extra queue packets between the kernels).
+template <typename K, typename... A>
+int launch_k(K kernel, dim3 grid, dim3 block, hipStream_t stream, const hipEvent_t* ev,
+             A... args) {
+    if (ev)
+        hipExtLaunchKernelGGL(kernel, grid, block, 0, stream, ev[0], ev[1], 0, args...);
+    else
+        kernel<<<grid, block, 0, stream>>>(args...);
+    return hipGetLastError() == hipSuccess ? RT_OK : RT_ERR_HIP;
+}
+
+// A profiled kernel slot that runs nothing: both events on the stream.
+int skip_k(hipStream_t stream, const hipEvent_t* ev) {
+    if (!ev) return RT_OK;
+    HIP_TRY(hipEventRecord(ev[0], stream));
+    HIP_TRY(hipEventRecord(ev[1], stream));
+    return RT_OK;
+}
+
 // Enqueue one render of rows [row_begin, row_end) on `stream`.  All scene
 // pointers are device pointers.
 int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origins,
@@ -853,43 +938,40 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
     if (path == RT_PATH_BINNED && !can_bin) return RT_ERR_UNSUPPORTED;
     const bool use_bin = path == RT_PATH_BINNED || (path == RT_PATH_AUTO && can_bin);
     if (used_path) *used_path = use_bin ? RT_PATH_BINNED : RT_PATH_GENERIC;
-    hipEvent_t* pe = nullptr;
+    const hipEvent_t* pe = nullptr;  // 6 events: prep, coarse, trace (start, stop)
     if (ctx->profile) {
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < 6; ++k) {
             hipEvent_t e;
             HIP_TRY(hipEventCreate(&e));
             ctx->prof_events.push_back(e);
         }
-        pe = &ctx->prof_events[ctx->prof_events.size() - 4];
-        HIP_TRY(hipEventRecord(pe[0], stream));
+        pe = &ctx->prof_events[ctx->prof_events.size() - 6];
         ++ctx->prof_count;
     }
+    const hipEvent_t* pe_prep = pe ? pe : nullptr;
+    const hipEvent_t* pe_coarse = pe ? pe + 2 : nullptr;
+    const hipEvent_t* pe_trace = pe ? pe + 4 : nullptr;
+    int rc;
     if (!use_bin) {
         const int64_t n = (int64_t)width * rows;
         const int64_t blocks = (n + kThreads - 1) / kThreads;
-        if (pe) {
-            HIP_TRY(hipEventRecord(pe[1], stream));
-            HIP_TRY(hipEventRecord(pe[2], stream));
-        }
-        generic_kernel<<<dim3((unsigned)blocks), dim3(kThreads), 0, stream>>>(
-            sd, dir, reinterpret_cast<const float4*>(origins), width, row_begin, row_end, fmt,
-            out);
-        HIP_TRY(hipGetLastError());
-        if (pe) HIP_TRY(hipEventRecord(pe[3], stream));
-        return RT_OK;
+        if ((rc = skip_k(stream, pe_prep)) || (rc = skip_k(stream, pe_coarse))) return rc;
+        return launch_k(generic_kernel, dim3((unsigned)blocks), dim3(kThreads), stream, pe_trace,
+                        sd, dir, reinterpret_cast<const float4*>(origins), width, row_begin,
+                        row_end, fmt, out);
     }
     const int n_tri = 12 * s->num_cubes;
     const int n_prims = n_tri + s->num_spheres;
-    const int n_bins_x = (width + kBinW - 1) / kBinW;
-    const int n_bins_y = (rows + kBinH - 1) / kBinH;
     const int n_cx = (width + kCoarse - 1) / kCoarse;
     const int n_cy = (rows + kCoarse - 1) / kCoarse;
-    const int64_t n_bins64 = (int64_t)n_bins_x * n_bins_y;
     const int64_t n_coarse64 = (int64_t)n_cx * n_cy;
-    if (n_bins64 >= (int64_t)1 << 31) return RT_ERR_INVALID_ARG;
-    const int n_bins = (int)n_bins64;
+    const int n_tiles_x = (width + kWaveTile - 1) / kWaveTile;
+    const int64_t n_tiles = (int64_t)n_tiles_x * ((rows + kWaveTileH - 1) / kWaveTileH);
+    if (n_tiles >= (int64_t)1 << 31 || n_coarse64 >= (int64_t)1 << 31) return RT_ERR_INVALID_ARG;
     const int n_coarse = (int)n_coarse64;
-    const int cap = n_prims > 0 ? n_prims : 1;
+    // per coarse bin: candidate ids, then their tile words (half_cap each,
+    // padded by 8 so the trace's 8-wide scalar reads stay inside the bin)
+    const int half_cap = (n_prims + 7) / 8 * 8 + 8;
 
     const size_t tri_off = 0;
     const size_t sph_off = align_up(sizeof(TriRec) * (size_t)n_tri, 256);
@@ -899,9 +981,9 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
     const size_t cnt_off =
         col_off + align_up(sizeof(float4) * (size_t)(s->num_cubes + s->num_spheres), 256);
     const size_t rec_need = cnt_off + align_up(sizeof(int) * (size_t)n_coarse, 256);
-    int rc = ensure(&ctx->rec_buf, &ctx->rec_cap, rec_need);
+    rc = ensure(&ctx->rec_buf, &ctx->rec_cap, rec_need);
     if (rc) return rc;
-    const size_t list_need = sizeof(int) * (size_t)cap * (size_t)n_coarse + 256;
+    const size_t list_need = sizeof(int) * 2 * (size_t)half_cap * (size_t)n_coarse + 256;
     rc = ensure(&ctx->list_buf, &ctx->list_cap, list_need);
     if (rc) return rc;
     char* base = static_cast<char*>(ctx->rec_buf);
@@ -919,28 +1001,26 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
     }
 
     if (n_prims > 0) {
-        prep_kernel<<<dim3((n_prims + kPrepThreads - 1) / kPrepThreads), dim3(kPrepThreads), 0,
-                      stream>>>(
-            sd, dir, width, row_begin, row_end, tri, sph, boxes, clsv, colours, ctx->flag,
-            ctx->gen);
-        HIP_TRY(hipGetLastError());
+        rc = launch_k(prep_kernel, dim3((n_prims + kPrepThreads - 1) / kPrepThreads),
+                      dim3(kPrepThreads), stream, pe_prep, sd, dir, width, row_begin, row_end,
+                      tri, sph, boxes, clsv, colours, ctx->flag, ctx->gen);
+        if (rc) return rc;
+        rc = launch_k(coarse3_kernel, dim3((unsigned)n_coarse), dim3(64), stream, pe_coarse,
+                      (const int4*)boxes, (const Cls*)clsv, n_prims, n_tri, n_cx, n_coarse,
+                      row_begin, half_cap, counts, lists);
+        if (rc) return rc;
+    } else {
+        if ((rc = skip_k(stream, pe_prep))) return rc;
+        HIP_TRY(hipMemsetAsync(counts, 0, sizeof(int) * (size_t)n_coarse, stream));
+        if ((rc = skip_k(stream, pe_coarse))) return rc;
     }
-    if (pe) HIP_TRY(hipEventRecord(pe[1], stream));
-    coarse_kernel<<<dim3((n_coarse + 3) / 4), dim3(kThreads), 0, stream>>>(
-        boxes, n_prims, n_cx, n_coarse, row_begin, cap, counts, lists);
-    HIP_TRY(hipGetLastError());
-    if (pe) HIP_TRY(hipEventRecord(pe[2], stream));
-    auto kern = ctx->trace_mode == 1 ? trace_kernel<1>
-              : ctx->trace_mode == 2 ? trace_kernel<2>
-              : ctx->trace_mode == 3 ? trace_kernel<3>
-              : ctx->trace_mode == 4 ? trace_kernel<4> : trace_kernel<0>;
-    kern<<<dim3((unsigned)n_bins), dim3(kThreads), 0, stream>>>(
-        sd, tri, sph, boxes, clsv, colours, counts, lists, cap, ctx->flag, ctx->gen, dir, width,
-        row_begin,
-        row_end, n_bins_x, n_cx, fmt, out);
-    HIP_TRY(hipGetLastError());
-    if (pe) HIP_TRY(hipEventRecord(pe[3], stream));
-    return RT_OK;
+    auto kern = ctx->trace_mode == 1 ? trace3_kernel<1>
+              : ctx->trace_mode == 2 ? trace3_kernel<2>
+              : ctx->trace_mode == 3 ? trace3_kernel<3> : trace3_kernel<0>;
+    return launch_k(kern, dim3((unsigned)n_tiles), dim3(64), stream, pe_trace, sd,
+                    (const TriRec*)tri, (const SphRec*)sph, (const float4*)colours,
+                    (const int*)counts, (const int*)lists, half_cap, (const unsigned*)ctx->flag,
+                    ctx->gen, dir, width, row_begin, row_end, n_tiles_x, n_cx, fmt, out);
 }
 
 }  // namespace
@@ -1105,11 +1185,12 @@ int rt_profile_read(rt_ctx* ctx, double* prep_ms, double* bin_ms, double* trace_
     if (!ctx) return RT_ERR_INVALID_ARG;
     HIP_TRY(hipSetDevice(ctx->device));
     double sums[3] = {0, 0, 0};
-    for (size_t q = 0; q + 3 < ctx->prof_events.size(); q += 4) {
-        HIP_TRY(hipEventSynchronize(ctx->prof_events[q + 3]));
+    for (size_t q = 0; q + 5 < ctx->prof_events.size(); q += 6) {
+        HIP_TRY(hipEventSynchronize(ctx->prof_events[q + 5]));
         for (int k = 0; k < 3; ++k) {
             float ms = 0.0f;
-            HIP_TRY(hipEventElapsedTime(&ms, ctx->prof_events[q + k], ctx->prof_events[q + k + 1]));
+            HIP_TRY(hipEventElapsedTime(&ms, ctx->prof_events[q + 2 * k],
+                                        ctx->prof_events[q + 2 * k + 1]));
             sums[k] += ms;
         }
     }
@@ -1171,10 +1252,20 @@ int rt_debug_triangle_box(const float v0[3], const float v1[3], const float v2[3
 
 // Diagnostics: select a trace-kernel ablation (0 = normal).
 int rt_debug_set_trace_mode(rt_ctx* ctx, int mode) {
-    if (!ctx || mode < 0 || mode > 4) return RT_ERR_INVALID_ARG;
+    if (!ctx || mode < 0 || mode > 3) return RT_ERR_INVALID_ARG;
     ctx->trace_mode = mode;
     return RT_OK;
 }
+
+#if RT_TIMELINE
+// Diagnostics build only: per-wave timeline buffer (8 x uint32 per wave).
+int rt_debug_set_timeline(rt_ctx* ctx, void* device_buf) {
+    if (!ctx) return RT_ERR_INVALID_ARG;
+    HIP_TRY(hipSetDevice(ctx->device));
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_timeline), &device_buf, sizeof(void*)));
+    return RT_OK;
+}
+#endif
 
 int rt_debug_tile_shape(int32_t* w, int32_t* h) {
     if (!w || !h) return RT_ERR_INVALID_ARG;

@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--cubes", type=int, default=64)
     ap.add_argument("--seed", type=int, default=3)
     ap.add_argument("--k", type=float, default=None)
+    ap.add_argument("--modes", default="0",
+                    help="comma list of trace-kernel ablation modes to time (0 = real)")
     args = ap.parse_args()
     import torch
     import __graft_entry__
@@ -72,17 +74,22 @@ def main():
             ref = frame
         elif not torch.equal(frame, ref):
             print(f"PARITY MISMATCH {name}: {(frame != ref).any(-1).sum().item()} px", flush=True)
-    times = {name: [] for name, _, _ in libs}
+    modes = [int(m) for m in args.modes.split(",")]
+    times = {f"{name}" + (f"/m{m}" if m else ""): [] for m in modes for name, _, _ in libs}
     for r in range(args.rounds):
         order = libs if r % 2 == 0 else libs[::-1]
-        for name, lib, ctx in order:
-            torch.cuda.synchronize()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-            run(lib, ctx, args.steps)
-            e1.record(stream)
-            torch.cuda.synchronize()
-            times[name].append(e0.elapsed_time(e1) / args.steps * 1e3)
+        for m in modes:
+            for name, lib, ctx in order:
+                lib.rt_debug_set_trace_mode(ctx, m)
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                run(lib, ctx, args.steps)
+                e1.record(stream)
+                torch.cuda.synchronize()
+                lib.rt_debug_set_trace_mode(ctx, 0)
+                times[f"{name}" + (f"/m{m}" if m else "")].append(
+                    e0.elapsed_time(e1) / args.steps * 1e3)
     res = {n: {"median_us": round(statistics.median(v), 2), "min_us": round(min(v), 2)}
            for n, v in times.items()}
     print(json.dumps(res, indent=1))

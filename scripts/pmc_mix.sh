@@ -10,7 +10,8 @@ i=0
 for grp in "SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_CVT SQ_INSTS_VALU_INT64" \
            "SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU" \
            "SQ_WAVES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY" \
-           "SQ_INSTS_SMEM SQ_INST_CYCLES_SMEM SQ_INST_LEVEL_SMEM SQ_INSTS_SALU SQ_INSTS_BRANCH SQ_IFETCH"; do
+           "SQ_INSTS_SMEM SQ_INST_CYCLES_SMEM SQ_INST_LEVEL_SMEM SQ_INSTS_SALU SQ_INSTS_BRANCH SQ_IFETCH" \
+           "SQ_INST_CYCLES_VALU SQ_INST_CYCLES_SALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_INSTS_LDS SQ_BUSY_CYCLES"; do
   i=$((i+1))
   (cd /tmp && timeout -k 10 200 rocprofv3 --kernel-trace --pmc $grp -d "$R/gpurun_out/${TAG}_$i" -o run --output-format csv -- \
       python "$R/bench.py" $ARGS > "$R/gpurun_out/${TAG}_$i.log" 2>&1)
@@ -22,7 +23,7 @@ d, tag = sys.argv[1], sys.argv[2]
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in glob.glob(f"{d}/{tag}_*/run_counter_collection.csv"):
     for r in csv.DictReader(open(f)):
-        if "trace_kernel" in r["Kernel_Name"]:
+        if "trace3_kernel" in r["Kernel_Name"] or "trace_kernel" in r["Kernel_Name"]:
             agg["trace"][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, v in sorted(agg["trace"].items()):
     print(f"{k:28s} {sum(v)/len(v):14.0f}")

@@ -1,0 +1,44 @@
+"""Per-launch HBM traffic of the trace kernel from scripts/pmc.sh's passes 1
+(WRITE_SIZE) and 2 (FETCH_SIZE), corrected as MI355X_MICROARCH.md's
+HBM/rocprofv3 section prescribes (KB units; FETCH_SIZE doubled on gfx950).
+Writes the JSON bench.py reads `roofline.traffic` from.
+
+    python scripts/pmc_traffic.py gpurun_out/pmc_r01 profiles/r01_pmc_config3.json
+"""
+import csv
+import json
+import re
+import sys
+
+KERNEL = re.compile(r"trace\d?_kernel<0>")
+
+
+def per_launch(path, counter):
+    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
+            if KERNEL.search(r["Kernel_Name"]) and r["Counter_Name"] == counter]
+    if not vals:
+        raise SystemExit(f"no {counter} rows for the trace kernel in {path}")
+    return sum(vals) / len(vals), len(vals)
+
+
+def main(prefix, out):
+    w_kb, nw = per_launch(f"{prefix}_1/run_counter_collection.csv", "WRITE_SIZE")
+    f_kb, nf = per_launch(f"{prefix}_2/run_counter_collection.csv", "FETCH_SIZE")
+    write_b = int(round(w_kb * 1024))
+    fetch_b = int(round(f_kb * 1024 * 2))
+    d = {"config": [4096, 4096, 256, 64, 3, "i32x4"],
+         "kernel": "trace3_kernel<0>",
+         "write_bytes_per_launch": write_b, "fetch_bytes_per_launch": fetch_b,
+         "hbm_bytes_per_launch": write_b + fetch_b,
+         "algo_bytes_per_launch": 4096 * 4096 * 16,
+         "launches": [nw, nf],
+         "method": "rocprofv3 --kernel-trace --pmc WRITE_SIZE and --pmc FETCH_SIZE in separate "
+                   "runs of bench.py --steps 10 --warmup 3 --no-cpu-baseline; KB x 1024; "
+                   "FETCH_SIZE doubled (gfx950 reports half of wide reads, "
+                   "MI355X_MICROARCH.md)"}
+    json.dump(d, open(out, "w"), indent=1)
+    print(json.dumps(d))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])

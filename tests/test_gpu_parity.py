@@ -242,9 +242,10 @@ def test_device_api_into_torch(pkg, rt):
     assert np.array_equal(out.cpu().numpy(), g["frame"])
 
 
-def test_candidate_lists_larger_than_lds_stage(pkg, rt, oracle):
-    """> kStage (512) candidates in one 64x64 coarse bin: the trace kernel
-    stages the list through LDS in several passes, order preserved."""
+def test_candidate_lists_larger_than_lds_round(pkg, rt, oracle):
+    """Hundreds of candidates in one 64x64 coarse bin: the coarse kernel
+    classifies them in several LDS rounds (kRound = 64) and the trace walks
+    them 8 at a time, the reference's primitive order preserved."""
     w, h = 100, 90
     scene = pkg.Scene.synthetic(w, h, 700, 40, seed=11, k=0.4)
     got, t = rt.render(scene, w, h)
