@@ -61,8 +61,15 @@ constexpr int kWaveTile = RT_TILE_W;                       // wave tile width
 constexpr int kRowsPerLane = RT_ROWS;
 constexpr int kLaneRows = 64 / RT_TILE_W;                  // lane rows per pass
 constexpr int kWaveTileH = kLaneRows * RT_ROWS;            // wave tile height
-constexpr int kCoarse = 64;       // coarse bin (candidate list) edge, pixels
-static_assert(kCoarse % kWaveTile == 0 && kCoarse % kWaveTileH == 0,
+#ifndef RT_COARSE_W
+#define RT_COARSE_W 64
+#endif
+#ifndef RT_COARSE_H
+#define RT_COARSE_H 64
+#endif
+constexpr int kCoarseW = RT_COARSE_W;  // coarse bin (candidate list) size, pixels
+constexpr int kCoarseH = RT_COARSE_H;
+static_assert(kCoarseW % kWaveTile == 0 && kCoarseH % kWaveTileH == 0,
               "wave tiles must tile a coarse bin");
 // prep_triangle's classifier margin covers tiles that overhang a box by up to
 // kTileSpan pixels on any side
@@ -603,9 +610,9 @@ __device__ __forceinline__ void shade_store(const float4* __restrict__ colours,
 
 
 
-// Tiles of one coarse bin: kCoarse / kWaveTile x kCoarse / kWaveTileH.
-constexpr int kTilesX = kCoarse / kWaveTile;
-constexpr int kTilesY = kCoarse / kWaveTileH;
+// Tiles of one coarse bin: kCoarseW / kWaveTile x kCoarseH / kWaveTileH.
+constexpr int kTilesX = kCoarseW / kWaveTile;
+constexpr int kTilesY = kCoarseH / kWaveTileH;
 static_assert(kTilesX * kTilesY <= 16, "two bits per tile in one 32-bit word");
 
 // Coarse binning with per-tile classification: one wave per coarse bin.
@@ -633,8 +640,8 @@ __global__ void __launch_bounds__(64) coarse3_kernel(
     __shared__ Cls s_cls[kRound];
     const int cb = blockIdx.x;
     const int lane = threadIdx.x;
-    const int x0 = (cb % n_cx) * kCoarse, x1 = x0 + kCoarse - 1;
-    const int y0 = row_begin + (cb / n_cx) * kCoarse, y1 = y0 + kCoarse - 1;
+    const int x0 = (cb % n_cx) * kCoarseW, x1 = x0 + kCoarseW - 1;
+    const int y0 = row_begin + (cb / n_cx) * kCoarseH, y1 = y0 + kCoarseH - 1;
     int* out_id = lists + (int64_t)cb * 2 * half_cap;
     int* out_tm = out_id + half_cap;
     int count = 0;   // appended to the output
@@ -726,23 +733,37 @@ __global__ void __launch_bounds__(64) coarse3_kernel(
 // One wave per kWaveTile x kWaveTileH tile, all candidate data on scalar
 // loads: count, then ids and tile words 8 at a time, then the records of
 // the candidates this tile keeps (in the reference's primitive order).
+#ifndef RT_TRACE_WG
+#define RT_TRACE_WG 1             // waves (tiles of one coarse bin) per trace workgroup
+#endif
+constexpr int kTraceWaves = RT_TRACE_WG;
+static_assert((kTilesX * kTilesY) % kTraceWaves == 0, "trace workgroup must tile a coarse bin");
+
 template <int kMode>
-__global__ void __launch_bounds__(64) RT_TRACE_ATTR trace3_kernel(
+__global__ void __launch_bounds__(64 * kTraceWaves) RT_TRACE_ATTR trace3_kernel(
     SceneDev scene, const TriRec* __restrict__ tri, const SphRec* __restrict__ sph,
     const float4* __restrict__ colours, const int* __restrict__ counts,
     const int* __restrict__ lists, int half_cap, const unsigned* __restrict__ nonfinite_flag,
     unsigned gen, float4 dir, int width, int row_begin, int row_end, int n_tiles_x, int n_cx,
     int out_format, void* __restrict__ out) {
-    const int tile = blockIdx.x;
-    const int lane = threadIdx.x;
-    const int rel_x = (tile % n_tiles_x) * kWaveTile;
-    const int rel_y = (tile / n_tiles_x) * kWaveTileH;  // relative to row_begin
+    // workgroup = kTraceWaves tiles of one coarse bin (independent waves on
+    // one CU: the candidate records one wave loads are scalar-cache hits for
+    // the others)
+    constexpr int kGroups = (kTilesX * kTilesY) / kTraceWaves;
+    const int cb = blockIdx.x / kGroups;
+    const int t = (blockIdx.x % kGroups) * kTraceWaves + (int)(threadIdx.x >> 6);
+#if RT_TIMELINE
+    const int tile = blockIdx.x * kTraceWaves + (int)(threadIdx.x >> 6);
+#endif
+    const int lane = threadIdx.x & 63;
+    const int rel_x = (cb % n_cx) * kCoarseW + (t % kTilesX) * kWaveTile;
+    const int rel_y = (cb / n_cx) * kCoarseH + (t / kTilesX) * kWaveTileH;  // vs row_begin
+    if (rel_x >= width || rel_y >= row_end - row_begin) return;  // wave-uniform
     const int tile_x = rel_x, tile_y = row_begin + rel_y;
     const int x = tile_x + (lane % kWaveTile);
     const int y0 = tile_y + (lane / kWaveTile);
     const int n_tri = 12 * scene.n_cubes;
-    const int cb = (rel_y / kCoarse) * n_cx + rel_x / kCoarse;
-    const int t = ((rel_y % kCoarse) / kWaveTileH) * kTilesX + (rel_x % kCoarse) / kWaveTile;
+    (void)n_tiles_x;
     TL_MARK(tl0);
 #if RT_TIMELINE
     const unsigned long long tlc0 = __builtin_amdgcn_s_memtime();
@@ -962,12 +983,12 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
     }
     const int n_tri = 12 * s->num_cubes;
     const int n_prims = n_tri + s->num_spheres;
-    const int n_cx = (width + kCoarse - 1) / kCoarse;
-    const int n_cy = (rows + kCoarse - 1) / kCoarse;
+    const int n_cx = (width + kCoarseW - 1) / kCoarseW;
+    const int n_cy = (rows + kCoarseH - 1) / kCoarseH;
     const int64_t n_coarse64 = (int64_t)n_cx * n_cy;
     const int n_tiles_x = (width + kWaveTile - 1) / kWaveTile;
-    const int64_t n_tiles = (int64_t)n_tiles_x * ((rows + kWaveTileH - 1) / kWaveTileH);
-    if (n_tiles >= (int64_t)1 << 31 || n_coarse64 >= (int64_t)1 << 31) return RT_ERR_INVALID_ARG;
+    const int64_t n_wgs = n_coarse64 * (kTilesX * kTilesY / kTraceWaves);
+    if (n_wgs >= (int64_t)1 << 31) return RT_ERR_INVALID_ARG;
     const int n_coarse = (int)n_coarse64;
     // per coarse bin: candidate ids, then their tile words (half_cap each,
     // padded by 8 so the trace's 8-wide scalar reads stay inside the bin)
@@ -1017,7 +1038,7 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
     auto kern = ctx->trace_mode == 1 ? trace3_kernel<1>
               : ctx->trace_mode == 2 ? trace3_kernel<2>
               : ctx->trace_mode == 3 ? trace3_kernel<3> : trace3_kernel<0>;
-    return launch_k(kern, dim3((unsigned)n_tiles), dim3(64), stream, pe_trace, sd,
+    return launch_k(kern, dim3((unsigned)n_wgs), dim3(64 * kTraceWaves), stream, pe_trace, sd,
                     (const TriRec*)tri, (const SphRec*)sph, (const float4*)colours,
                     (const int*)counts, (const int*)lists, half_cap, (const unsigned*)ctx->flag,
                     ctx->gen, dir, width, row_begin, row_end, n_tiles_x, n_cx, fmt, out);
