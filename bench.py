@@ -58,6 +58,11 @@ def parse():
                     help="diagnostics ablation: 1 = stores only, 2 = no per-pixel tests")
     ap.add_argument("--pmc", default=str(REPO / "profiles" / "r01_pmc_config3.json"),
                     help="committed PMC summary to read `traffic` from")
+    ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
+                    help="torch.distributed backend for N>1 (nccl = RCCL over xGMI)")
+    ap.add_argument("--rehearse", action="store_true",
+                    help="N>1 rehearsal on a 1-GPU box: every rank renders on cuda:0 and the "
+                         "collectives run over gloo on host copies")
     return ap.parse_args()
 
 
@@ -73,11 +78,18 @@ def main():
         if world == 1:
             raise SystemExit(f"--gpus {args.gpus} needs torchrun with {args.gpus} ranks")
     distributed = world > 1
+    backend = "gloo" if args.rehearse else args.backend
+    gpu = 0 if args.rehearse else local
     if distributed:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(gpu)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group("gloo")
+    dev = torch.device("cuda", gpu)
+    # collectives run on the GPU tensors with RCCL, on host copies with gloo
+    coll_dev = dev if backend == "nccl" else torch.device("cpu")
 
     pkg = __graft_entry__.load_package()
     w, rows = args.width, args.height
@@ -87,7 +99,7 @@ def main():
     scene = pkg.Scene.synthetic(w, full_h, n_sph, n_cub, seed=args.seed, k=k)
     rb, re = rank * rows, (rank + 1) * rows
 
-    rt = pkg.RayTracer(local)
+    rt = pkg.RayTracer(gpu)
     rt.set_trace_mode(args.trace_mode)
     t = {name: torch.from_numpy(np.ascontiguousarray(getattr(scene, name))).to(dev)
          for name in ("sphere_origins", "sphere_radius", "sphere_colours", "cube_vertices",
@@ -129,7 +141,7 @@ def main():
     wall_ms = (time.perf_counter() - t0) * 1e3 / args.steps
     event_ms = ev0.elapsed_time(ev1) / args.steps
     if distributed:
-        tt = torch.tensor([wall_ms], device=dev)
+        tt = torch.tensor([wall_ms], device=coll_dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         wall_ms = float(tt.item())
 
@@ -153,7 +165,7 @@ def main():
 
     traffic = None
     pmc_path = Path(args.pmc)
-    if pmc_path.exists():
+    if world == 1 and pmc_path.exists():  # measured for the 1-GPU workload only
         try:
             pmc = json.loads(pmc_path.read_text())
             if pmc.get("config") == [w, rows, args.spheres, args.cubes, args.seed, args.format]:
@@ -166,24 +178,26 @@ def main():
         # Texture assembly on rank 0 (north_star): one RCCL gather of the bands.
         from opencl_ray_tracer_amd import rowbands
 
+        band = out if coll_dev == dev else out.cpu()
         for _ in range(2):
-            rowbands.gather_frame(out, full_h, world, rank)
+            rowbands.gather_frame(band, full_h, world, rank)
         torch.cuda.synchronize(dev)
         barrier()
         g0 = time.perf_counter()
         reps = max(3, args.steps // 4)
         for _ in range(reps):
-            rowbands.gather_frame(out, full_h, world, rank)
+            rowbands.gather_frame(band, full_h, world, rank)
         torch.cuda.synchronize(dev)
         barrier()
         g_ms = (time.perf_counter() - g0) * 1e3 / reps
-        gather = {"collective": "rccl gather of row bands to rank 0", "ms": round(g_ms, 4),
+        gather = {"collective": f"{'rccl' if backend == 'nccl' else 'gloo (host)'} gather of "
+                                f"row bands to rank 0", "ms": round(g_ms, 4),
                   "bytes_to_root": algo_bytes * (world - 1),
                   "render_plus_gather_mrays": round(
                       world * rays_rank / ((wall_ms + g_ms) * 1e-3) / 1e6, 1)}
 
     cpu = None
-    if rank == 0 and not args.no_cpu_baseline:
+    if world == 1 and not args.no_cpu_baseline:  # rank 0 at N=1 only
         sys.path.insert(0, str(REPO / "tests"))
         from oracle_lib import Oracle  # CPU baseline only
 
@@ -209,7 +223,9 @@ def main():
                                    f"{args.cubes} cubes per rank, dense k={k:.2f}, seed {args.seed}",
                        "width": w, "rows_per_rank": rows, "image_height": full_h,
                        "spheres": n_sph, "cubes": n_cub, "format": args.format,
-                       "parallelism": f"row-bands x{world}"},
+                       "parallelism": f"row-bands x{world}"
+                                      + (" (rehearsal: shared cuda:0, gloo)" if args.rehearse
+                                         else "")},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "kernel": "trace3_kernel",
