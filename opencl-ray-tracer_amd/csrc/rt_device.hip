@@ -737,7 +737,12 @@ __global__ void __launch_bounds__(64) coarse3_kernel(
 #define RT_TRACE_WG 1             // waves (tiles of one coarse bin) per trace workgroup
 #endif
 constexpr int kTraceWaves = RT_TRACE_WG;
-static_assert((kTilesX * kTilesY) % kTraceWaves == 0, "trace workgroup must tile a coarse bin");
+#ifndef RT_TPW
+#define RT_TPW 1                  // tiles of one coarse bin traced in turn by one wave
+#endif
+constexpr int kTilesPerWave = RT_TPW;
+static_assert((kTilesX * kTilesY) % (kTraceWaves * kTilesPerWave) == 0,
+              "trace workgroups must tile a coarse bin");
 
 template <int kMode>
 __global__ void __launch_bounds__(64 * kTraceWaves) RT_TRACE_ATTR trace3_kernel(
@@ -749,25 +754,28 @@ __global__ void __launch_bounds__(64 * kTraceWaves) RT_TRACE_ATTR trace3_kernel(
     // workgroup = kTraceWaves tiles of one coarse bin (independent waves on
     // one CU: the candidate records one wave loads are scalar-cache hits for
     // the others)
-    constexpr int kGroups = (kTilesX * kTilesY) / kTraceWaves;
+    constexpr int kGroups = (kTilesX * kTilesY) / (kTraceWaves * kTilesPerWave);
     const int cb = blockIdx.x / kGroups;
-    const int t = (blockIdx.x % kGroups) * kTraceWaves + (int)(threadIdx.x >> 6);
+    const int wave_id = (blockIdx.x % kGroups) * kTraceWaves + (int)(threadIdx.x >> 6);
 #if RT_TIMELINE
     const int tile = blockIdx.x * kTraceWaves + (int)(threadIdx.x >> 6);
 #endif
     const int lane = threadIdx.x & 63;
-    const int rel_x = (cb % n_cx) * kCoarseW + (t % kTilesX) * kWaveTile;
-    const int rel_y = (cb / n_cx) * kCoarseH + (t / kTilesX) * kWaveTileH;  // vs row_begin
-    if (rel_x >= width || rel_y >= row_end - row_begin) return;  // wave-uniform
-    const int tile_x = rel_x, tile_y = row_begin + rel_y;
-    const int x = tile_x + (lane % kWaveTile);
-    const int y0 = tile_y + (lane / kWaveTile);
     const int n_tri = 12 * scene.n_cubes;
     (void)n_tiles_x;
     TL_MARK(tl0);
 #if RT_TIMELINE
     const unsigned long long tlc0 = __builtin_amdgcn_s_memtime();
 #endif
+#pragma unroll 1
+    for (int it = 0; it < kTilesPerWave; ++it) {
+    const int t = wave_id * kTilesPerWave + it;
+    const int rel_x = (cb % n_cx) * kCoarseW + (t % kTilesX) * kWaveTile;
+    const int rel_y = (cb / n_cx) * kCoarseH + (t / kTilesX) * kWaveTileH;  // vs row_begin
+    if (rel_x >= width || rel_y >= row_end - row_begin) continue;  // wave-uniform
+    const int tile_x = rel_x, tile_y = row_begin + rel_y;
+    const int x = tile_x + (lane % kWaveTile);
+    const int y0 = tile_y + (lane / kWaveTile);
 
     if (kMode == 0 && *nonfinite_flag == gen) {
         // Non-finite scene data: run the reference algorithm verbatim.
@@ -779,7 +787,7 @@ __global__ void __launch_bounds__(64 * kTraceWaves) RT_TRACE_ATTR trace3_kernel(
                 collide_generic(scene, make_float4((float)x, (float)y, 0.0f, 1.0f), dir);
             store_pixel(out, out_format, (int64_t)(y - row_begin) * width + x, p);
         }
-        return;
+        continue;
     }
 
     float closest[kRowsPerLane];
@@ -828,8 +836,9 @@ __global__ void __launch_bounds__(64 * kTraceWaves) RT_TRACE_ATTR trace3_kernel(
             }
         }
     }
-    TL_MARK(tl2);
     shade_store<kMode>(colours, closest, hit, x, y0, width, row_begin, row_end, out_format, out);
+    }  // tiles of this wave
+    TL_MARK(tl2);
 #if RT_TIMELINE
     {
         const unsigned tl3 = rt_now();
@@ -987,7 +996,7 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
     const int n_cy = (rows + kCoarseH - 1) / kCoarseH;
     const int64_t n_coarse64 = (int64_t)n_cx * n_cy;
     const int n_tiles_x = (width + kWaveTile - 1) / kWaveTile;
-    const int64_t n_wgs = n_coarse64 * (kTilesX * kTilesY / kTraceWaves);
+    const int64_t n_wgs = n_coarse64 * (kTilesX * kTilesY / (kTraceWaves * kTilesPerWave));
     if (n_wgs >= (int64_t)1 << 31) return RT_ERR_INVALID_ARG;
     const int n_coarse = (int)n_coarse64;
     // per coarse bin: candidate ids, then their tile words (half_cap each,

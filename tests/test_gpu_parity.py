@@ -224,6 +224,37 @@ def test_config3_full_frame(pkg, rt, oracle):
         assert np.array_equal(frame[r:r + 1], want), f"row {r}"
 
 
+def test_config5_style_4096_spheres(pkg, rt, oracle):
+    """Config 5's scene type (4096 spheres, no cubes) on a
+    2048^2 frame: long candidate lists per coarse bin (several coarse-kernel
+    LDS rounds), checked on a row sample, and band renders assemble to the
+    full frame."""
+    w = h = 2048
+    scene = pkg.Scene.synthetic(w, h, 4096, 0, seed=5, k=w / 640)
+    frame, t = rt.render(scene, w, h)
+    assert t.path == "binned"
+    for r in list(range(0, h, 173)) + [h - 1]:
+        want = oracle.trace(scene, w, h, rows=(r, r + 1), threads=THREADS)
+        assert np.array_equal(frame[r:r + 1], want), f"row {r}"
+    bands = [rt.render(scene, w, h, rows=(b, min(b + 700, h)))[0] for b in range(0, h, 700)]
+    assert np.array_equal(np.concatenate(bands), frame)
+
+
+def test_config4_style_band_of_8192_frame(pkg, rt, oracle):
+    """Config 4's layout: one rank's row band (rows 3072..4095 of an 8192^2
+    frame, 192 spheres + 64 cubes over the whole frame) rendered on its
+    own: band-relative tiles and coarse bins, primitives clamped to the
+    band."""
+    w = h = 8192
+    scene = pkg.Scene.synthetic(w, h, 192, 64, seed=4, k=w / 640)
+    rb, re = 3072, 4096
+    band, t = rt.render(scene, w, h, rows=(rb, re))
+    assert t.path == "binned" and band.shape == (re - rb, w, 4)
+    for r in list(range(rb, re, 97)) + [re - 1]:
+        want = oracle.trace(scene, w, h, rows=(r, r + 1), threads=THREADS)
+        assert np.array_equal(band[r - rb:r - rb + 1], want), f"row {r}"
+
+
 def test_device_api_into_torch(pkg, rt):
     """rt_render_device writing into a torch tensor on the current stream."""
     torch = pytest.importorskip("torch")
