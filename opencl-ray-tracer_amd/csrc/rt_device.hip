@@ -756,7 +756,10 @@ __global__ void __launch_bounds__(64 * kTraceWaves) RT_TRACE_ATTR trace3_kernel(
     // the others)
     constexpr int kGroups = (kTilesX * kTilesY) / (kTraceWaves * kTilesPerWave);
     const int cb = blockIdx.x / kGroups;
-    const int wave_id = (blockIdx.x % kGroups) * kTraceWaves + (int)(threadIdx.x >> 6);
+    // wave-uniform by construction; readfirstlane tells the compiler, so the
+    // per-candidate keep / inside bits stay in SGPRs (scalar branches)
+    const int wave_id = (blockIdx.x % kGroups) * kTraceWaves +
+                        __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
 #if RT_TIMELINE
     const int tile = blockIdx.x * kTraceWaves + (int)(threadIdx.x >> 6);
 #endif
