@@ -515,22 +515,43 @@ __device__ __forceinline__ void test_tri(const TriRec& r, int slot, bool inside,
     }
 }
 
+// Correctly rounded sqrtf for x in [2^-96, FLT_MAX]: v_sqrt_f32 plus the two
+// FMA residual corrections of the compiler's IEEE expansion, without its
+// denormal scaling and zero/inf fix-up (equal to sqrtf on every float of
+// that range: exhaustive check, scripts/check_sqrt.hip).
+__device__ __forceinline__ float sqrt_rn_normal(float x) {
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const int si = __builtin_bit_cast(int, s);
+    const float sm = __builtin_bit_cast(float, si - 1);
+    const float sp = __builtin_bit_cast(float, si + 1);
+    float r = __builtin_fmaf(-sm, s, x) <= 0.0f ? sm : s;
+    r = __builtin_fmaf(-sp, s, x) > 0.0f ? sp : r;
+    return r;
+}
+
 __device__ __forceinline__ void test_sph(const SphRec& s, int slot, float pxf, const float* pyf,
                                          float* closest, int* hit) {
-    {
-        const float lx = s.cx - pxf;
-        const float lx2 = lx * lx;
+    const float lx = s.cx - pxf;
+    const float lx2 = lx * lx;
+    float dist2[kRowsPerLane], arg[kRowsPerLane];
+    bool slow = false;
 #pragma unroll
-        for (int j = 0; j < kRowsPerLane; ++j) {
-            const float ly = s.cy - pyf[j];
-            const float a = lx2 + ly * ly;
-            const float dist2 = (a + s.kzw) - s.tca2;
-            const float thc = sqrtf(s.r2 - dist2);
-            const float t0 = s.tca - thc;
-            const bool take = !(dist2 > s.r2) & (t0 != 0.0f) & (t0 < closest[j]);
-            closest[j] = take ? t0 : closest[j];
-            hit[j] = take ? slot : hit[j];
-        }
+    for (int j = 0; j < kRowsPerLane; ++j) {
+        const float ly = s.cy - pyf[j];
+        const float a = lx2 + ly * ly;
+        dist2[j] = (a + s.kzw) - s.tca2;
+        arg[j] = s.r2 - dist2[j];
+        // a lane that can hit needs the general sqrtf outside [2^-96, FLT_MAX]
+        slow |= !(dist2[j] > s.r2) & !(arg[j] >= 0x1p-96f && arg[j] <= 3.40282347e38f);
+    }
+    const bool general = __ballot(slow) != 0ull;  // wave-uniform
+#pragma unroll
+    for (int j = 0; j < kRowsPerLane; ++j) {
+        const float thc = general ? sqrtf(arg[j]) : sqrt_rn_normal(arg[j]);
+        const float t0 = s.tca - thc;
+        const bool take = !(dist2[j] > s.r2) & (t0 != 0.0f) & (t0 < closest[j]);
+        closest[j] = take ? t0 : closest[j];
+        hit[j] = take ? slot : hit[j];
     }
 }
 
@@ -577,11 +598,23 @@ __device__ __forceinline__ void store_pixel(void* __restrict__ out, int out_form
 }
 
 // Shade (MainState.cpp:396-407) and store one lane's kRowsPerLane pixels.
-template <int kMode>
+// Pixel value of the Texture format (MainState.cpp:1026-1036) or int32x4.
+template <int kFmt>
+__device__ __forceinline__ void store_fmt(void* __restrict__ out, int64_t idx, int4v pix) {
+    if (kFmt == RT_FORMAT_I32X4)
+        reinterpret_cast<int4v*>(out)[idx] = pix;
+    else
+        reinterpret_cast<unsigned*>(out)[idx] = pack_rgba8(pix);
+}
+
+// Shade (MainState.cpp:396-407) and store one lane's kRowsPerLane pixels
+// (rows kLaneRows apart).  `full`: the whole wave tile lies inside the frame
+// band, so no per-lane bounds checks.
+template <int kMode, int kFmt>
 __device__ __forceinline__ void shade_store(const float4* __restrict__ colours,
                                             const float* closest, const int* hit, int x, int y0,
-                                            int width, int row_begin, int row_end,
-                                            int out_format, void* __restrict__ out) {
+                                            int width, int row_begin, int row_end, bool full,
+                                            void* __restrict__ out) {
     bool lane_hit = false;
 #pragma unroll
     for (int j = 0; j < kRowsPerLane; ++j) lane_hit |= hit[j] >= 0;
@@ -595,20 +628,27 @@ __device__ __forceinline__ void shade_store(const float4* __restrict__ colours,
         for (int j = 0; j < kRowsPerLane; ++j) col[j] = colours[hit[j] >= 0 ? hit[j] : 0];
 #pragma unroll
         for (int j = 0; j < kRowsPerLane; ++j) {
-            const int4v c = shade_hit(hit[j] >= 0 ? closest[j] : 0.0f, col[j]);
+            // lanes without a hit shade a dummy 1.0 (discarded) so that div180
+            // stays on its fast path
+            const int4v c = shade_hit(hit[j] >= 0 ? closest[j] : 1.0f, col[j]);
             if (hit[j] >= 0) pix[j] = c;
         }
     }
+    const int64_t idx0 = (int64_t)(y0 - row_begin) * width + x;
+    const int64_t row_step = (int64_t)kLaneRows * width;
 #pragma unroll
     for (int j = 0; j < kRowsPerLane; ++j) {
-        const int y = y0 + kLaneRows * j;
+        // kMode 3: everything but the stores (a store the compiler cannot drop)
         const bool store = kMode != 3 || pix[j].x == 0x7fffffff;
-        if (x < width && y < row_end && store)
-            store_pixel(out, out_format, (int64_t)(y - row_begin) * width + x, pix[j]);
+        if (full) {
+            if (store) store_fmt<kFmt>(out, idx0 + j * row_step, pix[j]);
+        } else {
+            const int y = y0 + kLaneRows * j;
+            if (x < width && y < row_end && store)
+                store_fmt<kFmt>(out, idx0 + j * row_step, pix[j]);
+        }
     }
 }
-
-
 
 // Tiles of one coarse bin: kCoarseW / kWaveTile x kCoarseH / kWaveTileH.
 constexpr int kTilesX = kCoarseW / kWaveTile;
@@ -744,7 +784,7 @@ constexpr int kTilesPerWave = RT_TPW;
 static_assert((kTilesX * kTilesY) % (kTraceWaves * kTilesPerWave) == 0,
               "trace workgroups must tile a coarse bin");
 
-template <int kMode>
+template <int kMode, int kFmt>
 __global__ void __launch_bounds__(64 * kTraceWaves) RT_TRACE_ATTR trace3_kernel(
     SceneDev scene, const TriRec* __restrict__ tri, const SphRec* __restrict__ sph,
     const float4* __restrict__ colours, const int* __restrict__ counts,
@@ -839,7 +879,8 @@ __global__ void __launch_bounds__(64 * kTraceWaves) RT_TRACE_ATTR trace3_kernel(
             }
         }
     }
-    shade_store<kMode>(colours, closest, hit, x, y0, width, row_begin, row_end, out_format, out);
+    const bool full = rel_x + kWaveTile <= width && tile_y + kWaveTileH <= row_end;
+    shade_store<kMode, kFmt>(colours, closest, hit, x, y0, width, row_begin, row_end, full, out);
     }  // tiles of this wave
     TL_MARK(tl2);
 #if RT_TIMELINE
@@ -1047,9 +1088,15 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
         HIP_TRY(hipMemsetAsync(counts, 0, sizeof(int) * (size_t)n_coarse, stream));
         if ((rc = skip_k(stream, pe_coarse))) return rc;
     }
-    auto kern = ctx->trace_mode == 1 ? trace3_kernel<1>
-              : ctx->trace_mode == 2 ? trace3_kernel<2>
-              : ctx->trace_mode == 3 ? trace3_kernel<3> : trace3_kernel<0>;
+    auto kern = fmt == RT_FORMAT_I32X4
+                    ? (ctx->trace_mode == 1   ? trace3_kernel<1, RT_FORMAT_I32X4>
+                       : ctx->trace_mode == 2 ? trace3_kernel<2, RT_FORMAT_I32X4>
+                       : ctx->trace_mode == 3 ? trace3_kernel<3, RT_FORMAT_I32X4>
+                                              : trace3_kernel<0, RT_FORMAT_I32X4>)
+                    : (ctx->trace_mode == 1   ? trace3_kernel<1, RT_FORMAT_RGBA8>
+                       : ctx->trace_mode == 2 ? trace3_kernel<2, RT_FORMAT_RGBA8>
+                       : ctx->trace_mode == 3 ? trace3_kernel<3, RT_FORMAT_RGBA8>
+                                              : trace3_kernel<0, RT_FORMAT_RGBA8>);
     return launch_k(kern, dim3((unsigned)n_wgs), dim3(64 * kTraceWaves), stream, pe_trace, sd,
                     (const TriRec*)tri, (const SphRec*)sph, (const float4*)colours,
                     (const int*)counts, (const int*)lists, half_cap, (const unsigned*)ctx->flag,

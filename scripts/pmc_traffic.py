@@ -10,7 +10,7 @@ import json
 import re
 import sys
 
-KERNEL = re.compile(r"trace\d?_kernel<0>")
+KERNEL = re.compile(r"trace\d?_kernel<0(, 0)?>")
 
 
 def per_launch(path, counter):
@@ -27,7 +27,7 @@ def main(prefix, out):
     write_b = int(round(w_kb * 1024))
     fetch_b = int(round(f_kb * 1024 * 2))
     d = {"config": [4096, 4096, 256, 64, 3, "i32x4"],
-         "kernel": "trace3_kernel<0>",
+         "kernel": "trace3_kernel<0, 0>",
          "write_bytes_per_launch": write_b, "fetch_bytes_per_launch": fetch_b,
          "hbm_bytes_per_launch": write_b + fetch_b,
          "algo_bytes_per_launch": 4096 * 4096 * 16,
