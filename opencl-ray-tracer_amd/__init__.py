@@ -24,7 +24,7 @@ __all__ = [
     "RT_ERR_UNSUPPORTED", "RT_FORMAT_I32X4", "RT_FORMAT_RGBA8", "RT_PATH_AUTO", "RT_PATH_BINNED",
     "RT_PATH_GENERIC", "RtError", "Scene", "Timing", "RayTracer", "MainState",
     "library", "library_path", "primary_ray_dir", "pack_rgba8", "cube_packed",
-    "deg_to_rad", "EXPORTED_SYMBOLS",
+    "deg_to_rad", "encode_png", "EXPORTED_SYMBOLS",
 ]
 
 PKG_DIR = Path(__file__).resolve().parent
@@ -302,16 +302,24 @@ class RayTracer:
 
     def render(self, scene: Scene, width: int, height: int, rows: Optional[Tuple[int, int]] = None,
                ray_dir: Optional[np.ndarray] = None, ray_origins: Optional[np.ndarray] = None,
-               fmt: str = "i32x4", path: str = "auto") -> Tuple[np.ndarray, Timing]:
+               fmt: str = "i32x4", path: str = "auto",
+               out: Optional[np.ndarray] = None) -> Tuple[np.ndarray, Timing]:
         """Synchronous host-buffer render (rt_render_path).  Returns the frame
-        (rows x width x 4 int32, or rows x width uint32 for rgba8)."""
+        (rows x width x 4 int32, or rows x width uint32 for rgba8), written
+        into `out` when given (a reused buffer, like the reference's
+        `pixels` vector, MainState.cpp:215, avoids first-touch page faults
+        in the readback)."""
         rb, re = rows if rows is not None else (0, height)
         d = primary_ray_dir() if ray_dir is None else np.ascontiguousarray(ray_dir, np.float32)
         org = None if ray_origins is None else np.ascontiguousarray(ray_origins, np.float32)
         if org is not None and org.size != 4 * width * height:
             raise ValueError("ray_origins must hold width*height float4")
         shape = (re - rb, width, 4) if fmt == "i32x4" else (re - rb, width)
-        out = np.empty(shape, np.int32 if fmt == "i32x4" else np.uint32)
+        dtype = np.int32 if fmt == "i32x4" else np.uint32
+        if out is None:
+            out = np.empty(shape, dtype)
+        elif out.shape != shape or out.dtype != dtype or not out.flags.c_contiguous:
+            raise ValueError(f"out must be a C-contiguous {dtype.__name__} array of {shape}")
         t = _Timing()
         sc = scene.as_c()
         _check(library().rt_render_path(self._ctx, ctypes.byref(sc), _ptr(d), _ptr(org), width,
@@ -387,6 +395,31 @@ def debug_sphere_prep(origin, radius, ray_dir, width, row_begin, row_end):
     return bool(ok), box, cls
 
 
+def encode_png(filename: str, rgba8: np.ndarray) -> None:
+    """Write an RGBA8 frame (uint32 H x W from pack_rgba8, or uint8 H x W x 4)
+    as an 8-bit RGBA PNG, the format lodepng::encode writes for the reference
+    (MainState.cpp:410-417).  Plain zlib, filter type 0 on every scanline."""
+    import struct
+    import zlib
+
+    px = np.ascontiguousarray(rgba8)
+    if px.dtype != np.uint8:
+        px = px.astype("<u4").view(np.uint8).reshape(px.shape[0], px.shape[1], 4)
+    h, w = px.shape[:2]
+    raw = np.zeros((h, 1 + 4 * w), np.uint8)
+    raw[:, 1:] = px.reshape(h, 4 * w)
+
+    def chunk(kind: bytes, data: bytes) -> bytes:
+        return (struct.pack(">I", len(data)) + kind + data +
+                struct.pack(">I", zlib.crc32(kind + data) & 0xFFFFFFFF))
+
+    png = (b"\x89PNG\r\n\x1a\n" +
+           chunk(b"IHDR", struct.pack(">IIBBBBB", w, h, 8, 6, 0, 0, 0)) +
+           chunk(b"IDAT", zlib.compress(raw.tobytes(), 6)) + chunk(b"IEND", b""))
+    with open(filename, "wb") as f:
+        f.write(png)
+
+
 class MainState:
     """Headless mirror of the reference's MainState trace flow
     (MainState.cpp:135-239 update, :419-639 scenes, :641 executeRayTracerOpenCL).
@@ -429,6 +462,11 @@ class MainState:
     def generate_image_from_pixels(self) -> np.ndarray:
         """RGBA8 Texture content (MainState.cpp:974-1045)."""
         return pack_rgba8(self.pixels.reshape(self.height, self.width, 4))
+
+    def encode_png(self, filename: str) -> None:
+        """MainState::encodePNG (MainState.cpp:410-417; the reference's call
+        site at :971 is commented out): the current frame as an RGBA8 PNG."""
+        encode_png(filename, self.generate_image_from_pixels())
 
     def close(self):
         self._rt.close()

@@ -198,3 +198,38 @@ def test_sphere_box_and_tile_classifier_are_conservative(pkg, oracle):
                 keep, _ = classify_tile(cls, False, tx, ty, tw, th)
                 if not keep:
                     assert not hits[ty:ty + th, tx:tx + tw].any(), (c, r, tx, ty)
+
+
+def _decode_png(path):
+    """Minimal decoder for the encoder's own output (8-bit RGBA, filter 0)."""
+    import struct
+    import zlib
+    data = open(path, "rb").read()
+    assert data[:8] == b"\x89PNG\r\n\x1a\n"
+    pos, idat, w, h = 8, b"", 0, 0
+    while pos < len(data):
+        n, = struct.unpack(">I", data[pos:pos + 4])
+        kind, body = data[pos + 4:pos + 8], data[pos + 8:pos + 8 + n]
+        crc, = struct.unpack(">I", data[pos + 8 + n:pos + 12 + n])
+        assert crc == zlib.crc32(kind + body) & 0xFFFFFFFF
+        if kind == b"IHDR":
+            w, h, depth, ctype = struct.unpack(">IIBB", body[:10])
+            assert (depth, ctype) == (8, 6)
+        elif kind == b"IDAT":
+            idat += body
+        pos += 12 + n
+    raw = np.frombuffer(zlib.decompress(idat), np.uint8).reshape(h, 1 + 4 * w)
+    assert not raw[:, 0].any()
+    return raw[:, 1:].reshape(h, w, 4)
+
+
+def test_encode_png_round_trip(pkg, oracle, tmp_path):
+    """MainState::encodePNG (MainState.cpp:410-417): the Texture's RGBA8
+    bytes survive the PNG round trip."""
+    frame = oracle.trace(oracle.scene_reference(1), 64, 48)
+    rgba = pkg.pack_rgba8(frame)
+    path = tmp_path / "ray.png"
+    pkg.encode_png(str(path), rgba)
+    got = _decode_png(str(path))
+    assert np.array_equal(got, rgba.astype("<u4").view(np.uint8).reshape(48, 64, 4))
+    assert (got[..., 3] == 255).all()
