@@ -2,6 +2,7 @@
 fixtures, bit-exact on the int32x4 frame (the reference's pixels vector,
 MainState.cpp:952-955).  Run on an MI355X with `pytest -m gpu`."""
 import os
+from pathlib import Path
 
 import numpy as np
 import pytest
@@ -283,3 +284,29 @@ def test_candidate_lists_larger_than_lds_round(pkg, rt, oracle):
     assert t.path == "binned"
     want = oracle.trace(scene, w, h, threads=THREADS)
     assert not diff_report(got, want), diff_report(got, want)
+
+
+@pytest.mark.parametrize("scene_id", [1, 2, 3])
+def test_headless_cpp_driver(pkg, scene_id, tmp_path):
+    """The C++ host (host/rt_headless.cpp: MainState's createSceneN +
+    executeRayTracerOpenCL flow through the C ABI) reproduces the golden
+    frame: its FNV-1a-64 line and its PPM Texture dump (MainState.cpp:
+    1026-1028 wrap)."""
+    import subprocess
+
+    exe = Path(pkg.library_path()).parent / "rt_headless"
+    if not exe.exists():
+        pytest.skip("rt_headless not built")
+    g = load_golden(f"scene{scene_id}_640x480")
+    ppm = tmp_path / "frame.ppm"
+    env = dict(os.environ)
+    env["LD_LIBRARY_PATH"] = str(exe.parent) + ":" + env.get("LD_LIBRARY_PATH", "")
+    r = subprocess.run([str(exe), "--scene", str(scene_id), "--seed", "1", "--ppm", str(ppm)],
+                       capture_output=True, text=True, env=env, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert f"fnv1a64 {int(g['fnv1a64']):016x}" in r.stdout, r.stdout
+    data = ppm.read_bytes()
+    header = b"P6\n640 480\n255\n"
+    assert data.startswith(header)
+    rgb = np.frombuffer(data[len(header):], np.uint8).reshape(480, 640, 3)
+    assert np.array_equal(rgb, g["frame"][..., :3].astype(np.uint8))
