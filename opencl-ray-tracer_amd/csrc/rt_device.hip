@@ -809,6 +809,7 @@ __global__ void __launch_bounds__(64 * kTraceWaves) RT_TRACE_ATTR trace3_kernel(
     TL_MARK(tl0);
 #if RT_TIMELINE
     const unsigned long long tlc0 = __builtin_amdgcn_s_memtime();
+    unsigned tl1 = 0, tl2 = 0;
 #endif
 #pragma unroll 1
     for (int it = 0; it < kTilesPerWave; ++it) {
@@ -850,7 +851,9 @@ __global__ void __launch_bounds__(64 * kTraceWaves) RT_TRACE_ATTR trace3_kernel(
     const int count = kMode == 1 ? 0 : counts[cb];
     const int* __restrict__ ids = lists + (int64_t)cb * 2 * half_cap;
     const int* __restrict__ tms = ids + half_cap;
-    TL_MARK(tl1);
+#if RT_TIMELINE
+    tl1 = rt_now();
+#endif
     for (int i0 = 0; i0 < count; i0 += 8) {
         int idv[8], tmv[8];
 #pragma unroll
@@ -880,9 +883,11 @@ __global__ void __launch_bounds__(64 * kTraceWaves) RT_TRACE_ATTR trace3_kernel(
         }
     }
     const bool full = rel_x + kWaveTile <= width && tile_y + kWaveTileH <= row_end;
+#if RT_TIMELINE
+    tl2 = rt_now();
+#endif
     shade_store<kMode, kFmt>(colours, closest, hit, x, y0, width, row_begin, row_end, full, out);
     }  // tiles of this wave
-    TL_MARK(tl2);
 #if RT_TIMELINE
     {
         const unsigned tl3 = rt_now();
