@@ -487,31 +487,35 @@ __device__ __forceinline__ unsigned rt_now() { return (unsigned)__builtin_amdgcn
 // the result, so the wave never diverges inside the walk.  The per-lane
 // (row-invariant) products are hoisted; each is the same fp64 operation on
 // the same operands as in MainState.cpp:257-298, so values are unchanged.
+#ifndef RT_ROWSKIP
+#define RT_ROWSKIP 0  // 1: skip triangle rows, 2: sphere rows, 3: both (no lane can hit)
+#endif
+
 __device__ __forceinline__ void test_tri(const TriRec& r, int slot, bool inside, double px,
                                          const double* py, float* closest, int* hit) {
-    {
-        const double tx = px - r.v0x;
-        const double txe1y = tx * r.e1y;               // q2 = tx*e1y - ty*e1x
-        const double q1 = r.k1 - tx * r.e1z;           // q1 = tz*e1x - tx*e1z
-        const double e2yq1 = r.e2y * q1;
-        const double txp0 = tx * r.p0;                 // u = (tx*p0 + ty*p1) * inv_det
+    const double tx = px - r.v0x;
+    const double txe1y = tx * r.e1y;               // q2 = tx*e1y - ty*e1x
+    const double q1 = r.k1 - tx * r.e1z;           // q1 = tz*e1x - tx*e1z
+    const double e2yq1 = r.e2y * q1;
+    const double txp0 = tx * r.p0;                 // u = (tx*p0 + ty*p1) * inv_det
 #pragma unroll
-        for (int j = 0; j < kRowsPerLane; ++j) {
-            const double ty = py[j] - r.v0y;
-            const double q2 = txe1y - ty * r.e1x;
-            const double q0 = ty * r.e1z - r.k0;
-            const double t = ((r.e2x * q0 + e2yq1) + r.e2z * q2) * r.inv_det;
-            const float tf = (float)t;
-            bool pass = true;
-            if (!inside) {  // wave-uniform
-                const double u = (txp0 + ty * r.p1) * r.inv_det;
-                const double v = (r.dz * q2) * r.inv_det;
-                pass = !((u < 0.0) | (u > 1.0) | (v < 0.0) | (u + v > 1.0));
-            }
-            const bool take = pass & (tf < closest[j]);
-            closest[j] = take ? tf : closest[j];
-            hit[j] = take ? slot : hit[j];
+    for (int j = 0; j < kRowsPerLane; ++j) {
+        const double ty = py[j] - r.v0y;
+        const double q2 = txe1y - ty * r.e1x;
+        bool pass = true;
+        if (!inside) {  // wave-uniform
+            const double u = (txp0 + ty * r.p1) * r.inv_det;
+            const double v = (r.dz * q2) * r.inv_det;
+            pass = !((u < 0.0) | (u > 1.0) | (v < 0.0) | (u + v > 1.0));
+            // no lane of this row inside the triangle: its t is never used
+            if ((RT_ROWSKIP & 1) && __ballot(pass) == 0ull) continue;
         }
+        const double q0 = ty * r.e1z - r.k0;
+        const double t = ((r.e2x * q0 + e2yq1) + r.e2z * q2) * r.inv_det;
+        const float tf = (float)t;
+        const bool take = pass & (tf < closest[j]);
+        closest[j] = take ? tf : closest[j];
+        hit[j] = take ? slot : hit[j];
     }
 }
 
@@ -547,6 +551,8 @@ __device__ __forceinline__ void test_sph(const SphRec& s, int slot, float pxf, c
     const bool general = __ballot(slow) != 0ull;  // wave-uniform
 #pragma unroll
     for (int j = 0; j < kRowsPerLane; ++j) {
+        // no lane of this row within the sphere's disc: nothing to update
+        if ((RT_ROWSKIP & 2) && __ballot(!(dist2[j] > s.r2)) == 0ull) continue;
         const float thc = general ? sqrtf(arg[j]) : sqrt_rn_normal(arg[j]);
         const float t0 = s.tca - thc;
         const bool take = !(dist2[j] > s.r2) & (t0 != 0.0f) & (t0 < closest[j]);
