@@ -117,9 +117,9 @@ def main():
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
 
-    def step():
-        rt.render_device(dscene, w, full_h, (rb, re), out.data_ptr(), fmt=args.format,
-                         stream=stream.cuda_stream)
+    # ctypes arguments built once; each step enqueues prep + coarse + trace
+    step = rt.bind_render_device(dscene, w, full_h, (rb, re), out.data_ptr(), fmt=args.format,
+                                 stream=stream.cuda_stream)
 
     def barrier():
         if distributed:

@@ -343,6 +343,31 @@ class RayTracer:
                                           _FORMATS[fmt], _PATHS[path], out_ptr, stream or None),
                "rt_render_device")
 
+    def bind_render_device(self, device_scene: dict, width: int, height: int,
+                           rows: Tuple[int, int], out_ptr: int,
+                           ray_dir: Optional[np.ndarray] = None, fmt: str = "i32x4",
+                           path: str = "auto", stream: int = 0, origins_ptr: int = 0):
+        """render_device with its ctypes arguments built once: returns a
+        zero-argument callable that enqueues the render (for per-frame loops
+        over an unchanged device scene / frame buffer)."""
+        d = primary_ray_dir() if ray_dir is None else np.ascontiguousarray(ray_dir, np.float32)
+        sc = _Scene(device_scene.get("sphere_origins"), device_scene.get("sphere_radius"),
+                    device_scene.get("sphere_colours"), int(device_scene.get("num_spheres", 0)),
+                    device_scene.get("cube_vertices"), device_scene.get("cube_colours"),
+                    int(device_scene.get("num_cubes", 0)), None, 0)
+        fn = library().rt_render_device
+        args = (self._ctx, ctypes.byref(sc), _ptr(d), ctypes.c_void_p(origins_ptr or None),
+                width, height, rows[0], rows[1], _FORMATS[fmt], _PATHS[path],
+                ctypes.c_void_p(out_ptr), ctypes.c_void_p(stream or None))
+        keep = (d, sc)  # referenced by the ctypes pointers above
+
+        def render() -> None:
+            rc = fn(*args)
+            if rc != RT_OK:
+                _check(rc, "rt_render_device")
+        render._keep = keep  # type: ignore[attr-defined]
+        return render
+
     def profile(self, enable: bool) -> None:
         _check(library().rt_profile_enable(self._ctx, int(enable)), "rt_profile_enable")
 
