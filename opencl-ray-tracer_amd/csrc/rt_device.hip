@@ -77,6 +77,9 @@ constexpr int kTileSpan = kWaveTile > kWaveTileH ? kWaveTile : kWaveTileH;
 static_assert(kTileSpan <= 64, "tile span");
 constexpr int kThreads = 256;
 constexpr int kPrepThreads = 64;  // prep: one wave per block, spread over CUs
+#ifndef RT_COMPACT
+#define RT_COMPACT 1              // band compaction: 0 never, 1 band renders, 2 always
+#endif
 constexpr double kEpsilon = 0.000001;      // MainState.cpp:15
 constexpr float kFar = 300000.0f;          // MainState.cpp:345
 
@@ -431,13 +434,23 @@ __global__ void __launch_bounds__(kThreads) generic_kernel(
 // ---------------------------------------------------------------------------
 // Binned path
 // ---------------------------------------------------------------------------
+// Band compaction (`live` != nullptr, band renders): the in-band primitives
+// (non-empty boxes) are listed in primitive order so that the coarse kernel
+// scans only them.  Each wave publishes a 64-bit ballot of its live lanes
+// with agent-scope (sc1) stores, drains them, and bumps `done`; the wave
+// that arrives last (no waiting anywhere) reads every chunk mask with sc1
+// loads, expands them into live_ids[], writes the count and resets `done`
+// for the next render.
 __global__ void __launch_bounds__(kPrepThreads) prep_kernel(
     SceneDev scene, float4 dir, int width, int row_begin, int row_end,
     TriRec* __restrict__ tri, SphRec* __restrict__ sph, int4* __restrict__ boxes,
     Cls* __restrict__ cls, float4* __restrict__ colours, unsigned* __restrict__ nonfinite_flag,
-    unsigned gen) {
+    unsigned gen, unsigned long long* chunk_masks, unsigned* done, int* __restrict__ live_ids,
+    int* __restrict__ n_live) {
     const int n_tri = 12 * scene.n_cubes;
+    const int n_prims = n_tri + scene.n_spheres;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x;
     Box b = empty_box();
     Cls k{};
     bool bad = false;
@@ -450,7 +463,7 @@ __global__ void __launch_bounds__(kPrepThreads) prep_kernel(
         prep_triangle(fa, fb, fc, (double)dir.x, (double)dir.y, (double)dir.z, width, row_begin,
                       row_end, &r, &b, &k, &bad);
         tri[i] = r;
-    } else if (i < n_tri + scene.n_spheres) {
+    } else if (i < n_prims) {
         const int s = i - n_tri;
         const float4 o = scene.sphere_origins[s];
         colours[scene.n_cubes + s] = scene.sphere_colours[s];
@@ -459,14 +472,46 @@ __global__ void __launch_bounds__(kPrepThreads) prep_kernel(
         prep_sphere(fo, scene.sphere_radius[s], dir.x, dir.y, dir.z, dir.w, width, row_begin,
                     row_end, &r, &b, &k, &bad);
         sph[s] = r;
-    } else {
-        return;
     }
-    boxes[i] = make_int4(b.x0, b.y0, b.x1, b.y1);
-    cls[i] = k;
-    if (bad) atomicMax(nonfinite_flag, gen);
-}
+    if (i < n_prims) {
+        boxes[i] = make_int4(b.x0, b.y0, b.x1, b.y1);
+        cls[i] = k;
+        if (bad) atomicMax(nonfinite_flag, gen);
+    }
+    if (!live_ids) return;
 
+    // ---- band compaction ----
+    const unsigned long long m = __ballot(i < n_prims && b.x0 <= b.x1);
+    if (lane == 0)
+        __hip_atomic_store(&chunk_masks[blockIdx.x], m, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the sc1 store has landed
+    unsigned prev = 0;
+    if (lane == 0) prev = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    prev = __shfl(prev, 0);
+    if (prev != gridDim.x - 1) return;  // not the last wave to arrive
+    const int n_chunks = (int)gridDim.x;
+    const unsigned long long below = (1ull << lane) - 1ull;
+    int base = 0;
+    for (int c0 = 0; c0 < n_chunks; c0 += 64) {
+        const unsigned long long mine =
+            c0 + lane < n_chunks ? __hip_atomic_load(&chunk_masks[c0 + lane], __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT)
+                                 : 0ull;
+        const int nc = min(64, n_chunks - c0);
+        for (int c = 0; c < nc; ++c) {
+            const unsigned lo = __builtin_amdgcn_readlane((unsigned)mine, c);
+            const unsigned hi = __builtin_amdgcn_readlane((unsigned)(mine >> 32), c);
+            const unsigned long long mc = ((unsigned long long)hi << 32) | lo;
+            if ((mc >> lane) & 1ull) live_ids[base + __popcll(mc & below)] = (c0 + c) * 64 + lane;
+            base += __popcll(mc);
+        }
+    }
+    if (lane == 0) {
+        *n_live = base;
+        __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
 
 #if RT_TIMELINE
 // per wave: realtime at entry / first staged / walked / stores issued,
@@ -678,8 +723,8 @@ static_assert(kTilesX * kTilesY <= 16, "two bits per tile in one 32-bit word");
 constexpr int kRound = RT_C3_ROUND;
 __global__ void __launch_bounds__(64) coarse3_kernel(
     const int4* __restrict__ boxes, const Cls* __restrict__ cls, int n_prims, int n_tri,
-    int n_cx, int n_coarse, int row_begin, int half_cap, int* __restrict__ counts,
-    int* __restrict__ lists) {
+    int n_cx, const int* __restrict__ live_ids, const int* __restrict__ n_live, int row_begin,
+    int half_cap, int* __restrict__ counts, int* __restrict__ lists) {
     __shared__ int s_ids[kRound];
     __shared__ unsigned s_tm[kRound];
     __shared__ int4 s_box[kRound];
@@ -740,13 +785,20 @@ __global__ void __launch_bounds__(64) coarse3_kernel(
         __builtin_amdgcn_wave_barrier();
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
     };
-    for (int base = 0; base < n_prims; base += 64 * kBatch) {
+    // scan all primitives, or (band renders) the compacted in-band list
+    const int n_scan = live_ids ? *n_live : n_prims;
+    for (int base = 0; base < n_scan; base += 64 * kBatch) {
         int4 bb[kBatch];
+        int pid[kBatch];
 #pragma unroll
         for (int k = 0; k < kBatch; ++k) {
-            const int p = base + 64 * k + lane;
-            bb[k] = p < n_prims ? boxes[p] : make_int4(1 << 30, 1 << 30, -(1 << 30), -(1 << 30));
+            const int e = base + 64 * k + lane;
+            pid[k] = e < n_scan ? (live_ids ? live_ids[e] : e) : -1;
         }
+#pragma unroll
+        for (int k = 0; k < kBatch; ++k)
+            bb[k] = pid[k] >= 0 ? boxes[pid[k]]
+                                : make_int4(1 << 30, 1 << 30, -(1 << 30), -(1 << 30));
 #pragma unroll
         for (int k = 0; k < kBatch; ++k) {
             const int4 b = bb[k];
@@ -761,7 +813,7 @@ __global__ void __launch_bounds__(64) coarse3_kernel(
             if (ov) {
                 const unsigned below = __builtin_amdgcn_mbcnt_hi(
                     (unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-                s_ids[staged + (int)below] = base + 64 * k + lane;
+                s_ids[staged + (int)below] = pid[k];
             }
             staged += n_ov;
         }
@@ -1011,8 +1063,8 @@ int skip_k(hipStream_t stream, const hipEvent_t* ev) {
 // Enqueue one render of rows [row_begin, row_end) on `stream`.  All scene
 // pointers are device pointers.
 int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origins,
-           int32_t width, int32_t row_begin, int32_t row_end, int32_t fmt, int32_t path,
-           void* out, hipStream_t stream, int32_t* used_path) {
+           int32_t width, int32_t row_begin, int32_t row_end, bool band, int32_t fmt,
+           int32_t path, void* out, hipStream_t stream, int32_t* used_path) {
     SceneDev sd{reinterpret_cast<const float4*>(s->sphere_origins), s->sphere_radius,
                 reinterpret_cast<const float4*>(s->sphere_colours),
                 reinterpret_cast<const float4*>(s->cube_vertices),
@@ -1065,7 +1117,10 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
     const size_t col_off = cls_off + align_up(sizeof(Cls) * (size_t)n_prims, 256);
     const size_t cnt_off =
         col_off + align_up(sizeof(float4) * (size_t)(s->num_cubes + s->num_spheres), 256);
-    const size_t rec_need = cnt_off + align_up(sizeof(int) * (size_t)n_coarse, 256);
+    const int n_chunks = (n_prims + kPrepThreads - 1) / kPrepThreads;
+    const size_t live_off = cnt_off + align_up(sizeof(int) * (size_t)n_coarse, 256);
+    const size_t mask_off = live_off + align_up(sizeof(int) * ((size_t)n_prims + 64), 256);
+    const size_t rec_need = mask_off + align_up(sizeof(unsigned long long) * (size_t)n_chunks, 256);
     rc = ensure(&ctx->rec_buf, &ctx->rec_cap, rec_need);
     if (rc) return rc;
     const size_t list_need = sizeof(int) * 2 * (size_t)half_cap * (size_t)n_coarse + 256;
@@ -1078,6 +1133,11 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
     Cls* clsv = reinterpret_cast<Cls*>(base + cls_off);
     float4* colours = reinterpret_cast<float4*>(base + col_off);
     int* counts = reinterpret_cast<int*>(base + cnt_off);
+    // band compaction workspace: n_live, then the ordered in-band ids
+    int* n_live = reinterpret_cast<int*>(base + live_off);
+    int* live_ids = n_live + 64;
+    unsigned long long* chunk_masks = reinterpret_cast<unsigned long long*>(base + mask_off);
+    const bool compact = (band && RT_COMPACT != 0) || RT_COMPACT == 2;
     int* lists = static_cast<int*>(ctx->list_buf);
     // generation-stamped non-finite flag: no per-launch memset needed
     if (++ctx->gen == 0) {
@@ -1086,13 +1146,15 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
     }
 
     if (n_prims > 0) {
-        rc = launch_k(prep_kernel, dim3((n_prims + kPrepThreads - 1) / kPrepThreads),
-                      dim3(kPrepThreads), stream, pe_prep, sd, dir, width, row_begin, row_end,
-                      tri, sph, boxes, clsv, colours, ctx->flag, ctx->gen);
+        rc = launch_k(prep_kernel, dim3((unsigned)n_chunks), dim3(kPrepThreads), stream, pe_prep,
+                      sd, dir, width, row_begin, row_end, tri, sph, boxes, clsv, colours,
+                      ctx->flag, ctx->gen, compact ? chunk_masks : nullptr, ctx->flag + 1,
+                      compact ? live_ids : nullptr, n_live);
         if (rc) return rc;
         rc = launch_k(coarse3_kernel, dim3((unsigned)n_coarse), dim3(64), stream, pe_coarse,
-                      (const int4*)boxes, (const Cls*)clsv, n_prims, n_tri, n_cx, n_coarse,
-                      row_begin, half_cap, counts, lists);
+                      (const int4*)boxes, (const Cls*)clsv, n_prims, n_tri, n_cx,
+                      (const int*)(compact ? live_ids : nullptr), (const int*)n_live, row_begin,
+                      half_cap, counts, lists);
         if (rc) return rc;
     } else {
         if ((rc = skip_k(stream, pe_prep))) return rc;
@@ -1149,8 +1211,9 @@ int rt_init(int device_ordinal, rt_ctx** out_ctx) {
             return RT_ERR_HIP;
         }
     }
-    if (hipMalloc(&ctx->flag, sizeof(unsigned)) != hipSuccess ||
-        hipMemset(ctx->flag, 0, sizeof(unsigned)) != hipSuccess) {
+    // [0] non-finite flag, [1] band-compaction arrival counter (zero between renders)
+    if (hipMalloc(&ctx->flag, 4 * sizeof(unsigned)) != hipSuccess ||
+        hipMemset(ctx->flag, 0, 4 * sizeof(unsigned)) != hipSuccess) {
         rt_destroy(ctx);
         return RT_ERR_OUT_OF_MEMORY;
     }
@@ -1222,8 +1285,8 @@ int rt_render_path(rt_ctx* ctx, const rt_scene* scene, const float ray_dir[4],
     dscene.cube_colours = reinterpret_cast<const float*>(sb + o_cc);
     HIP_TRY(hipEventRecord(ctx->ev[1], st));
     int32_t used = 0;
-    rc = launch(ctx, &dscene, ray_dir, d_origins, width, row_begin, row_end, out_format, path,
-                ctx->out_buf, st, &used);
+    rc = launch(ctx, &dscene, ray_dir, d_origins, width, row_begin, row_end,
+                row_begin > 0 || row_end < height, out_format, path, ctx->out_buf, st, &used);
     if (rc) return rc;
     HIP_TRY(hipEventRecord(ctx->ev[2], st));
     HIP_TRY(hipMemcpyAsync(host_out, ctx->out_buf, out_bytes, hipMemcpyDeviceToHost, st));
@@ -1262,7 +1325,7 @@ int rt_render_device(rt_ctx* ctx, const rt_scene* device_scene, const float ray_
     HIP_TRY(hipSetDevice(ctx->device));
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
     return launch(ctx, device_scene, ray_dir, device_ray_origins, width, row_begin, row_end,
-                  out_format, path, device_out, st, nullptr);
+                  row_begin > 0 || row_end < height, out_format, path, device_out, st, nullptr);
 }
 
 int rt_profile_enable(rt_ctx* ctx, int enable) {

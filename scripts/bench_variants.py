@@ -29,6 +29,9 @@ def main():
     ap.add_argument("--cubes", type=int, default=64)
     ap.add_argument("--seed", type=int, default=3)
     ap.add_argument("--k", type=float, default=None)
+    ap.add_argument("--ranks", type=int, default=1,
+                    help="render rank 0's band of a frame and scene scaled for this many ranks "
+                         "(bench.py's weak-scaling workload)")
     ap.add_argument("--modes", default="0",
                     help="comma list of trace-kernel ablation modes to time (0 = real)")
     args = ap.parse_args()
@@ -37,7 +40,9 @@ def main():
     pkg = __graft_entry__.load_package()
     w, h = args.width, args.height
     k = args.k if args.k is not None else w / 640
-    scene = pkg.Scene.synthetic(w, h, args.spheres, args.cubes, seed=args.seed, k=k)
+    full_h = h * args.ranks
+    scene = pkg.Scene.synthetic(w, full_h, args.spheres * args.ranks, args.cubes * args.ranks,
+                                seed=args.seed, k=k)
     dev = torch.device("cuda:0")
     t = {n: torch.from_numpy(np.ascontiguousarray(getattr(scene, n))).to(dev)
          for n in ("sphere_origins", "sphere_radius", "sphere_colours", "cube_vertices",
@@ -61,8 +66,8 @@ def main():
 
     def run(lib, ctx, n):
         for _ in range(n):
-            rc = lib.rt_render_device(ctx, ctypes.byref(sc), d.ctypes.data, None, w, h, 0, h, 0,
-                                      0, out.data_ptr(), stream.cuda_stream)
+            rc = lib.rt_render_device(ctx, ctypes.byref(sc), d.ctypes.data, None, w, full_h, 0,
+                                      h, 0, 0, out.data_ptr(), stream.cuda_stream)
             assert rc == 0
 
     ref = None

@@ -310,3 +310,22 @@ def test_headless_cpp_driver(pkg, scene_id, tmp_path):
     assert data.startswith(header)
     rgb = np.frombuffer(data[len(header):], np.uint8).reshape(480, 640, 3)
     assert np.array_equal(rgb, g["frame"][..., :3].astype(np.uint8))
+
+
+def test_band_compaction_weak_scaling_layout(pkg, rt, oracle):
+    """bench.py's N=8 weak-scaling layout at reduced size: a 1024 x 8192
+    frame with 8x the primitives, rendered as 8 row bands (band renders
+    compact the in-band primitives in prep; the arrival counter must reset
+    between renders) -- bit-identical to the full-frame render (no
+    compaction) and to the oracle on sampled rows."""
+    w, h, ranks = 1024, 8192, 8
+    scene = pkg.Scene.synthetic(w, h, 64 * ranks, 16 * ranks, seed=8, k=w / 640)
+    full, t = rt.render(scene, w, h)
+    assert t.path == "binned"
+    for r in range(ranks):
+        rb, re = r * h // ranks, (r + 1) * h // ranks
+        band, _ = rt.render(scene, w, h, rows=(rb, re))
+        assert np.array_equal(band, full[rb:re]), f"band {r}"
+    for row in range(0, h, 509):
+        want = oracle.trace(scene, w, h, rows=(row, row + 1), threads=THREADS)
+        assert np.array_equal(full[row:row + 1], want), f"row {row}"
