@@ -490,22 +490,28 @@ __global__ void __launch_bounds__(kPrepThreads) prep_kernel(
     if (lane == 0) prev = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     prev = __shfl(prev, 0);
     if (prev != gridDim.x - 1) return;  // not the last wave to arrive
+    // lane l expands chunk word c0 + l: wave prefix sum of the popcounts
+    // gives its output offset; the ids keep the primitive order
     const int n_chunks = (int)gridDim.x;
-    const unsigned long long below = (1ull << lane) - 1ull;
     int base = 0;
     for (int c0 = 0; c0 < n_chunks; c0 += 64) {
-        const unsigned long long mine =
+        unsigned long long mine =
             c0 + lane < n_chunks ? __hip_atomic_load(&chunk_masks[c0 + lane], __ATOMIC_RELAXED,
                                                      __HIP_MEMORY_SCOPE_AGENT)
                                  : 0ull;
-        const int nc = min(64, n_chunks - c0);
-        for (int c = 0; c < nc; ++c) {
-            const unsigned lo = __builtin_amdgcn_readlane((unsigned)mine, c);
-            const unsigned hi = __builtin_amdgcn_readlane((unsigned)(mine >> 32), c);
-            const unsigned long long mc = ((unsigned long long)hi << 32) | lo;
-            if ((mc >> lane) & 1ull) live_ids[base + __popcll(mc & below)] = (c0 + c) * 64 + lane;
-            base += __popcll(mc);
+        const int cnt = __popcll(mine);
+        int incl = cnt;  // inclusive scan over lanes
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int v = __shfl_up(incl, off);
+            if (lane >= off) incl += v;
         }
+        int pos = base + incl - cnt;
+        while (mine) {
+            live_ids[pos++] = (c0 + lane) * 64 + __builtin_ctzll(mine);
+            mine &= mine - 1ull;
+        }
+        base += __shfl(incl, 63);
     }
     if (lane == 0) {
         *n_live = base;
