@@ -19,6 +19,9 @@
  *   - cube packing: the reference's own Cube.cpp, compiled unmodified from
  *     /root/reference into oracle/_ref/libref_cube.so (oracle/Makefile),
  *     is compared vertex-for-vertex with orc_cube_* below.
+ *   - scene random numbers: the reference's own misc/Random.cpp, compiled
+ *     unmodified into oracle/_ref/libref_random.so, gives bit-identical
+ *     Random::getFloat streams to orc_get_float below.
  */
 #include "rt_oracle.h"
 
@@ -168,6 +171,11 @@ static float rnd(float mn, float mx) {
     float r = random * diff;
     return mn + r;
 }
+
+/* Test hooks: Random::init / Random::getFloat as restated above (pinned
+ * against the reference's own Random.cpp by tests/test_oracle.py). */
+void orc_srand(unsigned seed) { srand(seed); }
+float orc_get_float(float mn, float mx) { return rnd(mn, mx); }
 
 /* Three getFloat() calls that appear as arguments of one constructor call:
  * the C++ evaluation order is unspecified; rtl selects it. */

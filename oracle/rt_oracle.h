@@ -30,6 +30,10 @@ void orc_cube_rotate(float verts[144], float rx, float ry, float rz);     /* Cub
 void orc_cube_translate(float verts[144], float tx, float ty, float tz);  /* Cube.cpp:75-83 */
 float orc_deg2rad(float deg);                                             /* Utility.cpp:343-347 */
 
+/* Random::init / Random::getFloat (Random.cpp:10-42) on glibc rand(). */
+void orc_srand(unsigned seed);
+float orc_get_float(float mn, float mx);
+
 /* ---- the primary ray direction, MainState.cpp:37-39 ---- */
 void orc_ray_dir(float out[4]);
 

@@ -18,6 +18,7 @@ REPO = Path(__file__).resolve().parents[1]
 ORACLE_DIR = REPO / "oracle"
 LIB = ORACLE_DIR / "liboracle.so"
 REF_LIB = ORACLE_DIR / "_ref" / "libref_cube.so"
+REF_RANDOM_LIB = ORACLE_DIR / "_ref" / "libref_random.so"
 
 _vp, _i32, _f32 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_float
 
@@ -55,6 +56,8 @@ def _load() -> ctypes.CDLL:
         "orc_sphere_grid": (None, [_vp, _f32, _vp, _i32, _i32, _i32, _i32, _vp]),
         "orc_fnv1a_i32": (ctypes.c_uint64, [_vp, ctypes.c_int64]),
         "orc_pack_rgba8": (None, [_vp, ctypes.c_int64, _vp]),
+        "orc_srand": (None, [ctypes.c_uint]),
+        "orc_get_float": (_f32, [_f32, _f32]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -203,6 +206,21 @@ def ref_cube_lib() -> Optional[ctypes.CDLL]:
     lib = ctypes.CDLL(str(REF_LIB))
     lib.ref_cube_build.restype = ctypes.c_int
     lib.ref_cube_build.argtypes = [_vp, ctypes.c_int, _vp, _vp, _vp]
+    return lib
+
+
+def ref_random_lib() -> Optional[ctypes.CDLL]:
+    """oracle/_ref/libref_random.so: the reference's own Random.cpp (or None).
+    Loaded lazily: its Log::logW reference stays unbound (never called once
+    ref_random_init has run)."""
+    if not REF_RANDOM_LIB.exists():
+        return None
+    import os
+    lib = ctypes.CDLL(str(REF_RANDOM_LIB), mode=os.RTLD_LAZY)
+    lib.ref_random_init.restype = None
+    lib.ref_random_init.argtypes = [ctypes.c_uint]
+    lib.ref_random_get_float.restype = ctypes.c_float
+    lib.ref_random_get_float.argtypes = [ctypes.c_float, ctypes.c_float]
     return lib
 
 

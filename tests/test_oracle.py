@@ -141,3 +141,22 @@ def test_intersect_tri_no_t_positive_test(oracle):
     assert hit == 1 and t == -10.0
     hit, _ = oracle.intersect_tri([0, 0, 0], [0, 0, -1], [-5, -5, 0], [5, -5, 0], [10, -5, 0])
     assert hit == 0  # degenerate: det == 0
+
+
+def test_get_float_vs_reference_random_cpp(oracle):
+    """The scenes' random numbers (Random::init + Random::getFloat,
+    Random.cpp:10-42) against the reference's own Random.cpp compiled
+    unmodified (oracle/_ref/libref_random.so): same glibc rand() stream,
+    bit-identical floats, over the ranges createScene2/3 use."""
+    from oracle_lib import ref_random_lib
+    ref = ref_random_lib()
+    if ref is None:
+        pytest.skip("oracle/_ref not built (needs /root/reference)")
+    ranges = [(0.0, 630.0), (0.0, 470.0), (20.0, 100.0), (5.0, 30.0), (0.05, 1.0),
+              (0.0, 359.0), (30.0, 100.0), (-7.0, 7.0)]
+    for seed in (1, 2, 7, 12345):
+        ref.ref_random_init(seed)
+        want = [ref.ref_random_get_float(*ranges[i % len(ranges)]) for i in range(4000)]
+        oracle.lib.orc_srand(seed)
+        got = [oracle.lib.orc_get_float(*ranges[i % len(ranges)]) for i in range(4000)]
+        assert np.array_equal(np.float32(got), np.float32(want)), seed
