@@ -19,6 +19,7 @@ ORACLE_DIR = REPO / "oracle"
 LIB = ORACLE_DIR / "liboracle.so"
 REF_LIB = ORACLE_DIR / "_ref" / "libref_cube.so"
 REF_RANDOM_LIB = ORACLE_DIR / "_ref" / "libref_random.so"
+REF_GLM_LIB = ORACLE_DIR / "_ref" / "libref_glm.so"
 
 _vp, _i32, _f32 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_float
 
@@ -221,6 +222,20 @@ def ref_random_lib() -> Optional[ctypes.CDLL]:
     lib.ref_random_init.argtypes = [ctypes.c_uint]
     lib.ref_random_get_float.restype = ctypes.c_float
     lib.ref_random_get_float.argtypes = [ctypes.c_float, ctypes.c_float]
+    return lib
+
+
+def ref_glm_lib() -> Optional[ctypes.CDLL]:
+    """oracle/_ref/libref_glm.so: the reference's vendored glm (or None)."""
+    if not REF_GLM_LIB.exists():
+        return None
+    lib = ctypes.CDLL(str(REF_GLM_LIB))
+    lib.ref_glm_dot4.restype = ctypes.c_float
+    lib.ref_glm_dot4.argtypes = [_vp, _vp]
+    lib.ref_glm_ray_dir.restype = None
+    lib.ref_glm_ray_dir.argtypes = [_vp]
+    lib.ref_glm_sphere.restype = ctypes.c_float
+    lib.ref_glm_sphere.argtypes = [_vp, _vp, ctypes.c_float, _vp]
     return lib
 
 

@@ -160,3 +160,39 @@ def test_get_float_vs_reference_random_cpp(oracle):
         oracle.lib.orc_srand(seed)
         got = [oracle.lib.orc_get_float(*ranges[i % len(ranges)]) for i in range(4000)]
         assert np.array_equal(np.float32(got), np.float32(want)), seed
+
+
+def test_glm_arithmetic_vs_reference_glm(oracle):
+    """The oracle's glm restatements against the reference's vendored glm
+    0.9.6 (oracle/_ref/libref_glm.so): the primary ray direction
+    (MainState.cpp:37-39) and the sphere test's vec4 arithmetic
+    (MainState.cpp:300-327, glm::dot pairwise order), bit for bit."""
+    import ctypes
+    from oracle_lib import ref_glm_lib
+    ref = ref_glm_lib()
+    if ref is None:
+        pytest.skip("oracle/_ref not built (needs /root/reference)")
+    d = np.zeros(4, np.float32)
+    ref.ref_glm_ray_dir(d.ctypes.data)
+    assert np.array_equal(d.view(np.uint32), oracle.ray_dir().view(np.uint32))
+    rng = np.random.default_rng(17)
+    dirs = [RAY_DIR] + [rng.uniform(-1, 1, 4).astype(np.float32) for _ in range(3)]
+    n_hits = 0
+    for i in range(20000):
+        o = np.float32([rng.uniform(-50, 700), rng.uniform(-50, 500), rng.uniform(-5, 5), 1.0])
+        c = np.float32([rng.uniform(-50, 700), rng.uniform(-50, 500), -rng.uniform(0, 120),
+                        [1.0, 0.5, 3.0][i % 3]])
+        if i % 4 == 0:  # near-tangent: centre just off the ray through o
+            c[:2] = o[:2] + np.float32(rng.uniform(-3, 3, 2))
+        r = np.float32(rng.uniform(0.5, 60.0))
+        dv = np.ascontiguousarray(dirs[i % len(dirs)])
+        want = ref.ref_glm_sphere(o.ctypes.data, dv.ctypes.data, ctypes.c_float(r), c.ctypes.data)
+        got = oracle.intersect_sphere(o, dv, float(r), c)
+        assert np.float32(got).view(np.uint32) == np.float32(want).view(np.uint32), (o, c, r, dv)
+        n_hits += want != 0.0
+    assert n_hits > 1000
+    for _ in range(2000):
+        a, b = rng.uniform(-1e3, 1e3, (2, 4)).astype(np.float32)
+        want = ref.ref_glm_dot4(a.ctypes.data, b.ctypes.data)
+        got = ((a[0] * b[0]) + (a[1] * b[1])) + ((a[2] * b[2]) + (a[3] * b[3]))
+        assert np.float32(got) == np.float32(want)
