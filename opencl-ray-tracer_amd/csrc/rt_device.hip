@@ -75,7 +75,7 @@ static_assert(kCoarseW % kWaveTile == 0 && kCoarseH % kWaveTileH == 0,
 // kTileSpan pixels on any side
 constexpr int kTileSpan = kWaveTile > kWaveTileH ? kWaveTile : kWaveTileH;
 static_assert(kTileSpan <= 64, "tile span");
-constexpr int kThreads = 256;
+constexpr int kThreads = 256;       // generic_kernel block
 constexpr int kPrepThreads = 64;  // prep: one wave per block, spread over CUs
 #ifndef RT_COMPACT
 #define RT_COMPACT 1              // band compaction: 0 never, 1 band renders, 2 always
@@ -107,7 +107,7 @@ struct alignas(16) SphRec {
 };
 static_assert(sizeof(SphRec) == 32, "SphRec layout");
 
-// Per-primitive tile classifier (32 B, fp32, staged in LDS with the box).
+// Per-primitive tile classifier (32 B, fp32; evaluated by the coarse kernel).
 // Triangle: a = (v0x, v0y, au, bu), b = (av, bv, g, 0) with the exact
 // barycentrics u = au (x - v0x) + bu (y - v0y), v = av (x - v0x) + bv (y -
 // v0y) up to a margin g that also covers the fp64 rounding of the per-pixel
@@ -612,7 +612,7 @@ __device__ __forceinline__ void test_sph(const SphRec& s, int slot, float pxf, c
     }
 }
 
-// Tile classification of one staged candidate against the wave tile
+// Tile classification of one candidate against the wave tile
 // [x0, x0+kWaveTile-1] x [y0, y0+kWaveTileH-1] (fp32, conservative; see Cls).
 __device__ __forceinline__ void classify(const Cls& k, bool is_tri, float x0, float y0,
                                          bool* keep, bool* inside) {
