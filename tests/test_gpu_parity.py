@@ -329,3 +329,43 @@ def test_band_compaction_weak_scaling_layout(pkg, rt, oracle):
     for row in range(0, h, 509):
         want = oracle.trace(scene, w, h, rows=(row, row + 1), threads=THREADS)
         assert np.array_equal(full[row:row + 1], want), f"row {row}"
+
+
+def test_error_paths_on_device(pkg, rt):
+    """Status codes through the C ABI on a real device (rt_error_string
+    convention, MainState.cpp:1101-1179 replaced): forcing the binned path
+    on rays it cannot take is RT_ERR_UNSUPPORTED; bad sizes and rows are
+    RT_ERR_INVALID_ARG; the context stays usable afterwards."""
+    scene = pkg.Scene.reference(1, 1)
+    w, h = 64, 48
+    origins = np.zeros((h, w, 4), np.float32)
+    origins[..., 0], origins[..., 1] = np.meshgrid(np.arange(w), np.arange(h))
+    origins[..., 3] = 1.0
+    with pytest.raises(pkg.RtError) as e:
+        rt.render(scene, w, h, ray_origins=origins, path="binned")
+    assert e.value.status == pkg.RT_ERR_UNSUPPORTED
+    with pytest.raises(pkg.RtError) as e:
+        rt.render(scene, w, h, ray_dir=np.float32([0.3, 0.0, -1.0, -1.0]), path="binned")
+    assert e.value.status == pkg.RT_ERR_UNSUPPORTED
+    for rows in ((10, 10), (-1, 5), (0, h + 1)):
+        with pytest.raises(pkg.RtError) as e:
+            rt.render(scene, w, h, rows=rows)
+        assert e.value.status == pkg.RT_ERR_INVALID_ARG
+    # explicit origins equal to the implicit grid take the generic path and
+    # give the same frame as the binned one
+    frame, t = rt.render(scene, w, h)
+    same, t2 = rt.render(scene, w, h, ray_origins=origins)
+    assert (t.path, t2.path) == ("binned", "generic")
+    assert np.array_equal(frame, same)
+
+
+def test_very_many_primitives(pkg, rt, oracle):
+    """30,000 small spheres and 200 cubes on a 512^2 frame: hundreds of
+    candidates per coarse bin (many coarse-kernel rounds, long lists)."""
+    w = h = 512
+    scene = pkg.Scene.synthetic(w, h, 30000, 200, seed=21, k=0.3)
+    frame, t = rt.render(scene, w, h)
+    assert t.path == "binned"
+    for r in (0, 97, 255, 256, 400, 511):
+        want = oracle.trace(scene, w, h, rows=(r, r + 1), threads=THREADS)
+        assert np.array_equal(frame[r:r + 1], want), f"row {r}"
