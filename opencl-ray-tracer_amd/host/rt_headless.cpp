@@ -9,11 +9,18 @@
 //
 //   rt_headless [--scene 1|2|3] [--seed S] [--width W] [--height H]
 //               [--synthetic N M k] [--rows A B] [--ppm out.ppm] [--repeat R]
+//               [--bands B] [--devices D]
+//
+// --bands splits [A, B) into B row bands traced concurrently, one host
+// thread and one rt_ctx per band on device (band % D), each writing its rows
+// straight into the shared frame -- the reference's one pixels vector
+// (MainState.cpp:676) assembled by disjoint row ranges, SURVEY.md §8(e).
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "rt_hip.h"
@@ -44,6 +51,13 @@ bool write_ppm(const std::string& path, const std::vector<int32_t>& frame, int w
     return true;
 }
 
+struct Band {
+    int device = 0, row_begin = 0, row_end = 0;
+    rt_ctx* ctx = nullptr;
+    rt_timing timing{};
+    int status = RT_OK;
+};
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -52,6 +66,7 @@ int main(int argc, char** argv) {
     int syn_n = -1, syn_m = -1;
     float syn_k = 1.0f;
     int row_begin = 0, row_end = -1;
+    int n_bands = 1, n_devices = 1;
     std::string ppm;
     for (int i = 1; i < argc; ++i) {
         std::string a = argv[i];
@@ -75,12 +90,19 @@ int main(int argc, char** argv) {
             row_end = std::atoi(next());
         } else if (a == "--ppm") ppm = next();
         else if (a == "--repeat") repeat = std::atoi(next());
+        else if (a == "--bands") n_bands = std::atoi(next());
+        else if (a == "--devices") n_devices = std::atoi(next());
         else {
             std::fprintf(stderr, "unknown option %s\n", a.c_str());
             return 2;
         }
     }
     if (row_end < 0) row_end = height;
+    if (n_bands < 1 || n_devices < 1 || row_begin < 0 || row_end > height ||
+        row_begin >= row_end) {
+        std::fprintf(stderr, "bad --rows/--bands/--devices\n");
+        return 2;
+    }
 
     // Scene vectors, MainState.h:99-106 (cubes already flattened, :646-655).
     const int cap_s = syn_n >= 0 ? syn_n : 100, cap_c = syn_m >= 0 ? syn_m : 100;
@@ -102,35 +124,68 @@ int main(int argc, char** argv) {
         return 1;
     }
 
-    rt_ctx* ctx = nullptr;  // MainState ctor -> openCLInit (:52)
-    rc = rt_init(0, &ctx);
-    if (rc != RT_OK) {
-        std::fprintf(stderr, "rt_init failed: %s\n", rt_error_string(rc));
-        return 1;
+    // One context per band: MainState ctor -> openCLInit (:52).
+    const int rows = row_end - row_begin;
+    if (n_bands > rows) n_bands = rows;
+    std::vector<Band> bands(n_bands);
+    for (int b = 0; b < n_bands; ++b) {
+        Band& band = bands[b];
+        band.device = b % n_devices;
+        band.row_begin = row_begin + (int)((int64_t)rows * b / n_bands);
+        band.row_end = row_begin + (int)((int64_t)rows * (b + 1) / n_bands);
+        rc = rt_init(band.device, &band.ctx);
+        if (rc != RT_OK) {
+            std::fprintf(stderr, "rt_init(%d) failed: %s\n", band.device, rt_error_string(rc));
+            for (Band& o : bands) rt_destroy(o.ctx);
+            return 1;
+        }
     }
     float ray_dir[4];
     rt_primary_ray_dir(ray_dir);  // (0,0,-1,-1), MainState.cpp:37-39
     rt_scene scene{so.data(), sr.data(), sc.data(), ns, cv.data(), cc.data(), nc, nullptr, 0};
-    std::vector<int32_t> pixels(4 * (size_t)width * (row_end - row_begin));
-    rt_timing t{};
-    for (int r = 0; r < repeat; ++r) {
+    std::vector<int32_t> pixels(4 * (size_t)width * rows);
+    auto trace_band = [&](Band& band) {
+        int32_t* dst = pixels.data() + 4 * (size_t)width * (band.row_begin - row_begin);
+        band.status = rt_render(band.ctx, &scene, ray_dir, nullptr, width, height,
+                                band.row_begin, band.row_end, RT_FORMAT_I32X4, dst,
+                                &band.timing);
+    };
+    int status = 0;
+    for (int r = 0; r < repeat && status == 0; ++r) {
         std::printf("HIP Ray Tracer Begin\n");
-        rc = rt_render(ctx, &scene, ray_dir, nullptr, width, height, row_begin, row_end,
-                       RT_FORMAT_I32X4, pixels.data(), &t);
-        if (rc != RT_OK) {
-            std::fprintf(stderr, "rt_render failed: %s\n", rt_error_string(rc));
-            rt_destroy(ctx);
-            return 1;
+        if (n_bands == 1) {
+            trace_band(bands[0]);
+        } else {
+            std::vector<std::thread> workers;
+            for (Band& band : bands) workers.emplace_back(trace_band, std::ref(band));
+            for (std::thread& w : workers) w.join();
         }
-        std::printf("Time Taken: %.0f microseconds (upload %.1f, kernels %.1f, readback %.1f; %s path)\n",
-                    t.total_us, t.upload_us, t.kernel_us, t.download_us,
-                    t.path == RT_PATH_BINNED ? "binned" : "generic");
+        for (int b = 0; b < n_bands; ++b) {
+            const Band& band = bands[b];
+            if (band.status != RT_OK) {
+                std::fprintf(stderr, "rt_render failed (band %d): %s\n", b,
+                             rt_error_string(band.status));
+                status = 1;
+                continue;
+            }
+            const rt_timing& t = band.timing;
+            std::printf("Time Taken: %.0f microseconds (upload %.1f, kernels %.1f, readback %.1f; "
+                        "%s path)",
+                        t.total_us, t.upload_us, t.kernel_us, t.download_us,
+                        t.path == RT_PATH_BINNED ? "binned" : "generic");
+            if (n_bands > 1)
+                std::printf(" band %d rows [%d,%d) device %d", b, band.row_begin, band.row_end,
+                            band.device);
+            std::printf("\n");
+        }
     }
-    std::printf("frame %dx%d rows [%d,%d) spheres %d cubes %d fnv1a64 %016llx\n", width, height,
-                row_begin, row_end, ns, nc,
-                (unsigned long long)fnv1a(pixels.data(), pixels.size()));
-    if (!ppm.empty() && !write_ppm(ppm, pixels, width, row_end - row_begin))
-        std::fprintf(stderr, "could not write %s\n", ppm.c_str());
-    rt_destroy(ctx);
-    return 0;
+    if (status == 0) {
+        std::printf("frame %dx%d rows [%d,%d) spheres %d cubes %d fnv1a64 %016llx\n", width,
+                    height, row_begin, row_end, ns, nc,
+                    (unsigned long long)fnv1a(pixels.data(), pixels.size()));
+        if (!ppm.empty() && !write_ppm(ppm, pixels, width, rows))
+            std::fprintf(stderr, "could not write %s\n", ppm.c_str());
+    }
+    for (Band& band : bands) rt_destroy(band.ctx);
+    return status;
 }

@@ -312,6 +312,36 @@ def test_headless_cpp_driver(pkg, scene_id, tmp_path):
     assert np.array_equal(rgb, g["frame"][..., :3].astype(np.uint8))
 
 
+@pytest.mark.parametrize("bands", [3, 7])
+def test_headless_cpp_driver_bands(pkg, bands, tmp_path):
+    """rt_headless --bands: concurrent host threads, one rt_ctx each
+    (several contexts on the one device here), tracing ragged row bands
+    into the shared frame -- the same golden hash as the single render,
+    for the whole frame and for a sub-range of rows."""
+    import subprocess
+
+    exe = Path(pkg.library_path()).parent / "rt_headless"
+    if not exe.exists():
+        pytest.skip("rt_headless not built")
+    g = load_golden("scene3_640x480")
+    env = dict(os.environ)
+    env["LD_LIBRARY_PATH"] = str(exe.parent) + ":" + env.get("LD_LIBRARY_PATH", "")
+    base = [str(exe), "--scene", "3", "--seed", "1", "--repeat", "2", "--bands", str(bands)]
+    r = subprocess.run(base, capture_output=True, text=True, env=env, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert f"fnv1a64 {int(g['fnv1a64']):016x}" in r.stdout, r.stdout
+    assert r.stdout.count(" band ") == 2 * bands, r.stdout
+    ppm = tmp_path / "rows.ppm"
+    r = subprocess.run(base + ["--rows", "101", "333", "--ppm", str(ppm)],
+                       capture_output=True, text=True, env=env, timeout=120)
+    assert r.returncode == 0, r.stderr
+    data = ppm.read_bytes()
+    header = b"P6\n640 232\n255\n"
+    assert data.startswith(header)
+    rgb = np.frombuffer(data[len(header):], np.uint8).reshape(232, 640, 3)
+    assert np.array_equal(rgb, g["frame"][101:333, :, :3].astype(np.uint8))
+
+
 def test_band_compaction_weak_scaling_layout(pkg, rt, oracle):
     """bench.py's N=8 weak-scaling layout at reduced size: a 1024 x 8192
     frame with 8x the primitives, rendered as 8 row bands (band renders
