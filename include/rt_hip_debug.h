@@ -42,6 +42,11 @@ int rt_debug_tile_shape(int32_t* w, int32_t* h);
  * frames by design. */
 int rt_debug_set_trace_mode(rt_ctx* ctx, int mode);
 
+/* Byte budget for the coarse candidate lists (8 B x (primitives + 16) per
+ * 64x64 bin); binned frames over it render as internal row bands.
+ * 0 restores the default (4 GiB). */
+int rt_debug_set_list_budget(rt_ctx* ctx, int64_t bytes);
+
 #ifdef __cplusplus
 }
 #endif

@@ -131,6 +131,7 @@ def library() -> ctypes.CDLL:
         "rt_debug_triangle_box": (ctypes.c_int, [vp, vp, vp, vp, i32, i32, i32, vp, vp]),
         "rt_debug_sphere_box": (ctypes.c_int, [vp, f32, vp, i32, i32, i32, vp, vp]),
         "rt_debug_set_trace_mode": (ctypes.c_int, [vp, ctypes.c_int]),
+        "rt_debug_set_list_budget": (ctypes.c_int, [vp, ctypes.c_int64]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -381,6 +382,11 @@ class RayTracer:
     def set_trace_mode(self, mode: int) -> None:
         """Diagnostics ablation of the trace kernel (0 = normal)."""
         _check(library().rt_debug_set_trace_mode(self._ctx, mode), "rt_debug_set_trace_mode")
+
+    def set_list_budget(self, nbytes: int) -> None:
+        """Diagnostics: coarse-list byte budget (0 = default); frames over it
+        render as internal row bands."""
+        _check(library().rt_debug_set_list_budget(self._ctx, nbytes), "rt_debug_set_list_budget")
 
     def device_info(self) -> dict:
         name = ctypes.create_string_buffer(256)

@@ -417,18 +417,20 @@ __device__ inline int4v collide_generic(const SceneDev& s, float4 origin, float4
 __global__ void __launch_bounds__(kThreads) generic_kernel(
     SceneDev scene, float4 dir, const float4* __restrict__ origins, int width,
     int row_begin, int row_end, int out_format, void* __restrict__ out) {
+    // grid-stride: the AQL grid counts work-items in 32 bits, frames may not
     const int64_t n = (int64_t)width * (row_end - row_begin);
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int x = (int)(i % width);
-    const int y = row_begin + (int)(i / width);
-    const float4 o = origins ? origins[(int64_t)y * width + x]
-                             : make_float4((float)x, (float)y, 0.0f, 1.0f);
-    const int4v p = collide_generic(scene, o, dir);
-    if (out_format == RT_FORMAT_I32X4)
-        reinterpret_cast<int4v*>(out)[i] = p;
-    else
-        reinterpret_cast<unsigned*>(out)[i] = pack_rgba8(p);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const int x = (int)(i % width);
+        const int y = row_begin + (int)(i / width);
+        const float4 o = origins ? origins[(int64_t)y * width + x]
+                                 : make_float4((float)x, (float)y, 0.0f, 1.0f);
+        const int4v p = collide_generic(scene, o, dir);
+        if (out_format == RT_FORMAT_I32X4)
+            reinterpret_cast<int4v*>(out)[i] = p;
+        else
+            reinterpret_cast<unsigned*>(out)[i] = pack_rgba8(p);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -992,6 +994,9 @@ struct rt_ctx {
     unsigned* flag = nullptr;   // non-finite scene flag (generation-stamped)
     unsigned gen = 0;
     int trace_mode = 0;  // diagnostics ablation, see trace3_kernel
+    // coarse lists take 8 B x (primitives + 16) per 64x64 bin; a frame whose
+    // lists would exceed this is rendered as internal row bands
+    int64_t list_budget = (int64_t)4 << 30;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     // profiling: per render, start/stop events of the prep, coarse and trace
     // kernels, attached to the kernels' own dispatch packets
@@ -1081,6 +1086,26 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
     if (path == RT_PATH_BINNED && !can_bin) return RT_ERR_UNSUPPORTED;
     const bool use_bin = path == RT_PATH_BINNED || (path == RT_PATH_AUTO && can_bin);
     if (used_path) *used_path = use_bin ? RT_PATH_BINNED : RT_PATH_GENERIC;
+    if (use_bin) {
+        // Bound the candidate-list workspace: split into bands of whole
+        // coarse rows, each a band render (prep compacts to its primitives),
+        // in order on the same stream.
+        const int64_t n_prims = 12 * (int64_t)s->num_cubes + s->num_spheres;
+        const int64_t row_bytes = 8 * ((n_prims + 7) / 8 * 8 + 8) * ((width + kCoarseW - 1) / kCoarseW);
+        const int64_t n_cy = (rows + kCoarseH - 1) / kCoarseH;
+        if (n_cy > 1 && row_bytes * n_cy > ctx->list_budget) {
+            const int64_t per = std::max<int64_t>(1, ctx->list_budget / row_bytes) * kCoarseH;
+            const size_t px_bytes = fmt == RT_FORMAT_I32X4 ? 16 : 4;
+            for (int64_t rb = row_begin; rb < row_end; rb += per) {
+                const int32_t re = (int32_t)std::min<int64_t>(rb + per, row_end);
+                char* dst = static_cast<char*>(out) + (size_t)(rb - row_begin) * width * px_bytes;
+                const int rc = launch(ctx, s, d, origins, width, (int32_t)rb, re, true, fmt, path,
+                                      dst, stream, nullptr);
+                if (rc) return rc;
+            }
+            return RT_OK;
+        }
+    }
     const hipEvent_t* pe = nullptr;  // 6 events: prep, coarse, trace (start, stop)
     if (ctx->profile) {
         for (int k = 0; k < 6; ++k) {
@@ -1097,7 +1122,7 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
     int rc;
     if (!use_bin) {
         const int64_t n = (int64_t)width * rows;
-        const int64_t blocks = (n + kThreads - 1) / kThreads;
+        const int64_t blocks = std::min<int64_t>((n + kThreads - 1) / kThreads, (int64_t)1 << 20);
         if ((rc = skip_k(stream, pe_prep)) || (rc = skip_k(stream, pe_coarse))) return rc;
         return launch_k(generic_kernel, dim3((unsigned)blocks), dim3(kThreads), stream, pe_trace,
                         sd, dir, reinterpret_cast<const float4*>(origins), width, row_begin,
@@ -1110,7 +1135,8 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
     const int64_t n_coarse64 = (int64_t)n_cx * n_cy;
     const int n_tiles_x = (width + kWaveTile - 1) / kWaveTile;
     const int64_t n_wgs = n_coarse64 * (kTilesX * kTilesY / (kTraceWaves * kTilesPerWave));
-    if (n_wgs >= (int64_t)1 << 31) return RT_ERR_INVALID_ARG;
+    // one trace work-item per 64 x kTraceWaves; AQL grid sizes are 32-bit
+    if (n_wgs * 64 * kTraceWaves > (int64_t)UINT32_MAX) return RT_ERR_INVALID_ARG;
     const int n_coarse = (int)n_coarse64;
     // per coarse bin: candidate ids, then their tile words (half_cap each,
     // padded by 8 so the trace's 8-wide scalar reads stay inside the bin)
@@ -1411,6 +1437,12 @@ int rt_debug_triangle_box(const float v0[3], const float v1[3], const float v2[3
 }
 
 // Diagnostics: select a trace-kernel ablation (0 = normal).
+int rt_debug_set_list_budget(rt_ctx* ctx, int64_t bytes) {
+    if (!ctx || bytes < 0) return RT_ERR_INVALID_ARG;
+    ctx->list_budget = bytes ? bytes : (int64_t)4 << 30;
+    return RT_OK;
+}
+
 int rt_debug_set_trace_mode(rt_ctx* ctx, int mode) {
     if (!ctx || mode < 0 || mode > 3) return RT_ERR_INVALID_ARG;
     ctx->trace_mode = mode;

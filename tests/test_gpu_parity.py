@@ -399,3 +399,93 @@ def test_very_many_primitives(pkg, rt, oracle):
     for r in (0, 97, 255, 256, 400, 511):
         want = oracle.trace(scene, w, h, rows=(r, r + 1), threads=THREADS)
         assert np.array_equal(frame[r:r + 1], want), f"row {r}"
+
+
+def _shifted(pkg, scene, dx=0.0, dy=0.0):
+    """The scene translated by (dx, dy) in float32, as the host would
+    store it (cube vertices already world-space, MainState.cpp:646-655)."""
+    so = scene.sphere_origins.copy()
+    so[:, 0] += np.float32(dx)
+    so[:, 1] += np.float32(dy)
+    cv = scene.cube_vertices.copy()
+    cv[:, :, 0] += np.float32(dx)
+    cv[:, :, 1] += np.float32(dy)
+    return pkg.Scene(so, scene.sphere_radius, scene.sphere_colours, cv, scene.cube_colours)
+
+
+@pytest.mark.parametrize("w,h", [(1 << 24, 1), (1 << 21, 3), (3, 1 << 21)])
+def test_extreme_aspect_frames(pkg, rt, oracle, w, h):
+    """The ABI's coordinate limit (2^24, the last width at which float
+    pixel coordinates are exact) and extreme aspect ratios: one coarse row
+    of up to 262,144 bins, or one coarse column of 32,768. Primitives sit
+    at the far end of the long axis. Whole frame against the oracle, and
+    binned == generic."""
+    base = pkg.Scene.synthetic(min(w, 4096), min(h, 4096), 240, 24, seed=5, k=1.0)
+    scene = _shifted(pkg, base, dx=max(w - 4096, 0), dy=max(h - 4096, 0))
+    got, t = rt.render(scene, w, h)
+    assert t.path == "binned"
+    gen, t = rt.render(scene, w, h, path="generic")
+    assert t.path == "generic"
+    assert np.array_equal(got, gen)
+    if w % 4096 == 0:
+        # the oracle splits work by rows: give it the same rays as explicit
+        # origins (exact integers below 2^24) folded into 4096-wide rows
+        ys, xs = np.divmod(np.arange(w * h, dtype=np.int64), w)
+        org = np.stack([xs, ys, np.zeros_like(xs), np.ones_like(xs)], -1).astype(np.float32)
+        want = oracle.trace(scene, 4096, w * h // 4096, ray_origins=org,
+                            threads=THREADS).reshape(h, w, 4)
+    else:
+        want = oracle.trace(scene, w, h, threads=THREADS)
+    assert not diff_report(got, want), diff_report(got, want)
+    assert (got[..., 0] != 0).sum() > 1000  # the far end really is drawn
+
+
+def test_maximum_size_frames(pkg, rt, oracle):
+    """A 16384 x 16400 frame (268.7 M rays, past the generic kernel's
+    2^28-thread grid, so its grid-stride loop runs twice) in RGBA8 on both
+    paths, bit-equal; and a 16384^2 int32x4 frame (4 GiB) on sampled rows
+    against the oracle."""
+    w = 16384
+    scene = pkg.Scene.synthetic(w, w, 256, 64, seed=9, k=w / 640)
+    a, t = rt.render(scene, w, 16400, fmt="rgba8")
+    assert t.path == "binned"
+    b, t = rt.render(scene, w, 16400, fmt="rgba8", path="generic")
+    assert t.path == "generic"
+    assert np.array_equal(a, b)
+    del b
+    rows = [0, 4095, 8191, 12288, 16383, 16399]
+    want = oracle.trace_rows(scene, w, 16400, rows, threads=THREADS)
+    assert np.array_equal(a[rows], oracle.pack_rgba8(want))
+    del a
+    full, t = rt.render(scene, w, w)
+    assert t.path == "binned"
+    want = oracle.trace_rows(scene, w, w, rows[:-1], threads=THREADS)
+    assert np.array_equal(full[rows[:-1]], want)
+
+
+def test_list_budget_bands(pkg, rt, oracle):
+    """Frames whose coarse candidate lists would pass the workspace budget
+    render as internal bands of whole coarse rows (band renders, compacted
+    prep), one after another on the stream: bit-identical to the unsplit
+    frame, for full frames, row ranges and both formats."""
+    w, h = 1000, 777
+    scene = pkg.Scene.synthetic(w, h, 500, 40, seed=31, k=1.2)
+    full, t = rt.render(scene, w, h)
+    assert t.path == "binned"
+    full8, _ = rt.render(scene, w, h, fmt="rgba8")
+    n_prims = 12 * 40 + 500
+    row_bytes = 8 * ((n_prims + 7) // 8 * 8 + 8) * ((w + 63) // 64)
+    try:
+        for budget in (1, 2 * row_bytes, 5 * row_bytes + 1):
+            rt.set_list_budget(budget)
+            got, t = rt.render(scene, w, h)
+            assert t.path == "binned"
+            assert np.array_equal(got, full), budget
+            got, _ = rt.render(scene, w, h, rows=(50, 700))
+            assert np.array_equal(got, full[50:700]), budget
+            got, _ = rt.render(scene, w, h, fmt="rgba8")
+            assert np.array_equal(got, full8), budget
+    finally:
+        rt.set_list_budget(0)
+    want = oracle.trace(scene, w, h, threads=THREADS)
+    assert not diff_report(full, want), diff_report(full, want)
