@@ -1,0 +1,63 @@
+"""Frames in flight: K renders of the bench's config-3 frame spread round-robin
+over S (context, stream, frame buffer) slots, S = 1, 2, 3, interleaved
+rounds; prints µs per frame.  Every slot's frame is checked bit-exact
+against the single-stream frame."""
+import argparse
+import statistics
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+REPO = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(REPO))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--slots", default="1,2,3")
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--size", type=int, default=4096)
+    args = ap.parse_args()
+    import torch
+    import __graft_entry__
+    pkg = __graft_entry__.load_package()
+    w = h = args.size
+    scene = pkg.Scene.synthetic(w, h, 256, 64, seed=3, k=w / 640)
+    dev = torch.device("cuda:0")
+    t = {n: torch.from_numpy(np.ascontiguousarray(getattr(scene, n))).to(dev)
+         for n in ("sphere_origins", "sphere_radius", "sphere_colours", "cube_vertices",
+                   "cube_colours")}
+    ds = {n: v.data_ptr() for n, v in t.items()}
+    ds["num_spheres"], ds["num_cubes"] = scene.num_spheres, scene.num_cubes
+    slots = [int(s) for s in args.slots.split(",")]
+    smax = max(slots)
+    ctxs = [pkg.RayTracer(0) for _ in range(smax)]
+    streams = [torch.cuda.Stream(dev) for _ in range(smax)]
+    outs = [torch.empty((h, w, 4), dtype=torch.int32, device=dev) for _ in range(smax)]
+    fns = [ctxs[i].bind_render_device(ds, w, h, (0, h), outs[i].data_ptr(),
+                                      stream=streams[i].cuda_stream) for i in range(smax)]
+    res = {s: [] for s in slots}
+    for r in range(args.rounds):
+        for s in slots:
+            for i in range(2 * s):
+                fns[i % s]()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for i in range(args.steps):
+                fns[i % s]()
+            torch.cuda.synchronize()
+            res[s].append((time.perf_counter() - t0) / args.steps * 1e6)
+    ref = outs[0].cpu()
+    for i in range(1, smax):
+        assert torch.equal(outs[i].cpu(), ref), f"slot {i} differs"
+    for s in slots:
+        med = statistics.median(res[s])
+        print(f"slots {s}: {med:.1f} us/frame  {w * h / med / 1e3:.1f} Grays/s  "
+              f"(min {min(res[s]):.1f})")
+
+
+if __name__ == "__main__":
+    main()
