@@ -722,6 +722,10 @@ static_assert(kTilesX * kTilesY <= 16, "two bits per tile in one 32-bit word");
 // into the candidate's LDS word; (3) candidates kept by some tile are
 // appended in order.  Output: counts[cb]; ids at lists[cb * 2 * half_cap
 // ...] and tile words at lists[cb * 2 * half_cap + half_cap ...].
+#ifndef RT_C3_ABL
+#define RT_C3_ABL 0  // diagnostics only: 1 = box scan + compaction, nothing classified or listed;
+                     // 2 = as 1, every wave reading the same 64 boxes (L1-resident)
+#endif
 #ifndef RT_C3_ROUND
 #define RT_C3_ROUND 64
 #endif
@@ -805,7 +809,7 @@ __global__ void __launch_bounds__(64) coarse3_kernel(
         }
 #pragma unroll
         for (int k = 0; k < kBatch; ++k)
-            bb[k] = pid[k] >= 0 ? boxes[pid[k]]
+            bb[k] = pid[k] >= 0 ? boxes[RT_C3_ABL == 2 ? (pid[k] & 63) : pid[k]]
                                 : make_int4(1 << 30, 1 << 30, -(1 << 30), -(1 << 30));
 #pragma unroll
         for (int k = 0; k < kBatch; ++k) {
@@ -815,7 +819,7 @@ __global__ void __launch_bounds__(64) coarse3_kernel(
             const int n_ov = __popcll(m);
             if (n_ov == 0) continue;
             if (staged + n_ov > kRound) {
-                classify_round(staged);
+                if (RT_C3_ABL == 0) classify_round(staged);  // diag: 1 = scan only
                 staged = 0;
             }
             if (ov) {
@@ -826,7 +830,8 @@ __global__ void __launch_bounds__(64) coarse3_kernel(
             staged += n_ov;
         }
     }
-    if (staged) classify_round(staged);
+    if (staged && RT_C3_ABL == 0) classify_round(staged);
+    if (RT_C3_ABL != 0 && lane == 0) out_tm[0] = staged;  // keep the scan; lists stay empty
     if (lane == 0) counts[cb] = count;
 }
 
