@@ -101,9 +101,11 @@ static_assert(sizeof(TriRec) == 128, "TriRec layout");
 // Per-sphere constants of the binned path (32 B).  With dir = (0, 0, D, Dw)
 // and origins (x, y, 0, 1): tca = dot4(L, d) and the z/w half of dot4(L, L)
 // do not depend on the pixel (MainState.cpp:300-327, glm pairwise dot).
+// `fast` (1 or 0): every lane that can hit gets an r2 - dist2 in
+// {0} u [2^-94, 2^102], where sqrt_rn_normal equals sqrtf (see prep_sphere).
 struct alignas(16) SphRec {
     float cx, cy, kzw, tca2;  // kzw = Lz*Lz + Lw*Lw, tca2 = tca*tca
-    float r2, tca, pad0, pad1;
+    float r2, tca, fast, pad1;
 };
 static_assert(sizeof(SphRec) == 32, "SphRec layout");
 
@@ -263,7 +265,13 @@ __host__ __device__ inline void prep_sphere(const float* o, float radius, float 
     rec->tca2 = tca2;
     rec->r2 = r2;
     rec->tca = tca;
-    rec->pad0 = rec->pad1 = 0.0f;
+    // r2 >= 2^-70: a hitting lane has dist2 <= r2, so r2 - dist2 is 0, or
+    // >= r2 / 2 (dist2 <= r2 / 2), or an exact nonzero difference of floats
+    // >= r2 / 2, a multiple of ulp(2^-71) = 2^-94.  The 2^100 caps keep
+    // dist2 >= -2^101, so r2 - dist2 <= 2^102 (and tca2 finite).
+    rec->fast = (r2 >= 0x1p-70f && r2 <= 0x1p100f && fabsf(tca2) <= 0x1p100f &&
+                 fabsf(kzw) <= 0x1p100f) ? 1.0f : 0.0f;
+    rec->pad1 = 0.0f;
     (void)dx;
     (void)dy;
     if (*nonfinite || !(tca >= 0.0f)) return;  // tca < 0 (or NaN): never a hit
@@ -591,17 +599,16 @@ __device__ __forceinline__ void test_sph(const SphRec& s, int slot, float pxf, c
     const float lx = s.cx - pxf;
     const float lx2 = lx * lx;
     float dist2[kRowsPerLane], arg[kRowsPerLane];
-    bool slow = false;
 #pragma unroll
     for (int j = 0; j < kRowsPerLane; ++j) {
         const float ly = s.cy - pyf[j];
         const float a = lx2 + ly * ly;
         dist2[j] = (a + s.kzw) - s.tca2;
         arg[j] = s.r2 - dist2[j];
-        // a lane that can hit needs the general sqrtf outside [2^-96, FLT_MAX]
-        slow |= !(dist2[j] > s.r2) & !(arg[j] >= 0x1p-96f && arg[j] <= 3.40282347e38f);
     }
-    const bool general = __ballot(slow) != 0ull;  // wave-uniform
+    // per sphere (scalar): the general sqrtf only where a hitting lane's
+    // argument could leave the range sqrt_rn_normal is exact on
+    const bool general = !(s.fast != 0.0f);
 #pragma unroll
     for (int j = 0; j < kRowsPerLane; ++j) {
         // no lane of this row within the sphere's disc: nothing to update

@@ -5,7 +5,9 @@
 //  (b) rt_device.hip's sqrt_rn_normal(x) (v_sqrt_f32 + the two FMA residual
 //      corrections, without the denormal scaling and the zero/inf fix-up)
 //      for every x in [2^-96, FLT_MAX] -- the domain the trace kernel uses
-//      it on.
+//      it on;
+//  (c) sqrt_rn_normal at +0 (an argument r2 - dist2 == 0 reaches it when a
+//      pixel lies exactly on a sphere's rim), +inf and NaN.
 #include <hip/hip_runtime.h>
 #include <cstdio>
 
@@ -26,6 +28,13 @@ __global__ void check(unsigned long long* bad, unsigned* first) {
         const unsigned ref = __builtin_bit_cast(unsigned, sqrtf(x));
         if (__builtin_bit_cast(unsigned, (float)__builtin_amdgcn_sqrt((double)x)) != ref)
             atomicAdd(&bad[0], 1ull);
+        if (i == 0u || i == 0x7f800000u) {  // (c): +0 -> +0, +inf -> +inf
+            if (__builtin_bit_cast(unsigned, sqrt_rn_normal(x)) != ref) atomicAdd(&bad[2], 1ull);
+        }
+        if (i == 0x7f800000u) {  // (c): NaN stays NaN
+            const float n = sqrt_rn_normal(__builtin_bit_cast(float, 0x7fc00000u));
+            if (n == n) atomicAdd(&bad[2], 1ull);
+        }
         if (i >= 0x0f800000u && i < 0x7f800000u &&
             __builtin_bit_cast(unsigned, sqrt_rn_normal(x)) != ref) {
             atomicAdd(&bad[1], 1ull);
@@ -37,16 +46,17 @@ __global__ void check(unsigned long long* bad, unsigned* first) {
 int main() {
     unsigned long long* d;
     unsigned* f;
-    if (hipMalloc(&d, 16) != hipSuccess || hipMalloc(&f, 4) != hipSuccess) return 2;
-    (void)hipMemset(d, 0, 16);
+    if (hipMalloc(&d, 24) != hipSuccess || hipMalloc(&f, 4) != hipSuccess) return 2;
+    (void)hipMemset(d, 0, 24);
     (void)hipMemset(f, 0xff, 4);
     check<<<4096, 256>>>(d, f);
-    unsigned long long h[2];
+    unsigned long long h[3];
     unsigned hf;
-    (void)hipMemcpy(h, d, 16, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(h, d, 24, hipMemcpyDeviceToHost);
     (void)hipMemcpy(&hf, f, 4, hipMemcpyDeviceToHost);
     printf("(a) f64 route: %llu mismatches over all non-negative floats\n", h[0]);
     printf("(b) sqrt_rn_normal: %llu mismatches over [2^-96, FLT_MAX] (first 0x%08x)\n", h[1],
            h[1] ? hf : 0u);
-    return h[1] == 0 ? 0 : 1;
+    printf("(c) sqrt_rn_normal at +0, +inf, NaN: %llu mismatches\n", h[2]);
+    return h[1] == 0 && h[2] == 0 ? 0 : 1;
 }
