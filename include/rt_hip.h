@@ -115,7 +115,10 @@ int rt_render_path(rt_ctx* ctx, const rt_scene* scene, const float ray_dir[4],
  * row-band driver and the benchmark): every pointer in `device_scene`,
  * `device_ray_origins` and `device_out` is a device pointer on the context's
  * device, `stream` is a hipStream_t (NULL = the context's stream).
- * Asynchronous: work is enqueued on `stream` and the call returns. */
+ * Asynchronous: work is enqueued on `stream` and the call returns.
+ * Renders on one context share its workspace (primitive records, candidate
+ * lists): enqueue them on one stream, or synchronise before switching
+ * streams.  Concurrent renders need one context each. */
 int rt_render_device(rt_ctx* ctx, const rt_scene* device_scene,
                      const float ray_dir[4], const float* device_ray_origins,
                      int32_t width, int32_t height, int32_t row_begin,

@@ -1108,6 +1108,7 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
         if (n_cy > 1 && row_bytes * n_cy > ctx->list_budget) {
             const int64_t per = std::max<int64_t>(1, ctx->list_budget / row_bytes) * kCoarseH;
             const size_t px_bytes = fmt == RT_FORMAT_I32X4 ? 16 : 4;
+            const int32_t prof_count0 = ctx->prof_count;
             for (int64_t rb = row_begin; rb < row_end; rb += per) {
                 const int32_t re = (int32_t)std::min<int64_t>(rb + per, row_end);
                 char* dst = static_cast<char*>(out) + (size_t)(rb - row_begin) * width * px_bytes;
@@ -1115,6 +1116,7 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
                                       dst, stream, nullptr);
                 if (rc) return rc;
             }
+            if (ctx->profile) ctx->prof_count = prof_count0 + 1;  // one render, summed bands
             return RT_OK;
         }
     }

@@ -485,7 +485,15 @@ def test_list_budget_bands(pkg, rt, oracle):
             assert np.array_equal(got, full[50:700]), budget
             got, _ = rt.render(scene, w, h, fmt="rgba8")
             assert np.array_equal(got, full8), budget
+        # profiling counts the banded frame as one render, its bands summed
+        rt.set_list_budget(2 * row_bytes)
+        rt.profile(True)
+        rt.render(scene, w, h)
+        prof = rt.profile_read()
+        rt.profile(False)
+        assert prof["renders"] == 1 and prof["trace_ms"] > 0, prof
     finally:
+        rt.profile(False)
         rt.set_list_budget(0)
     want = oracle.trace(scene, w, h, threads=THREADS)
     assert not diff_report(full, want), diff_report(full, want)
