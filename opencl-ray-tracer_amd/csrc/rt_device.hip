@@ -103,9 +103,12 @@ static_assert(sizeof(TriRec) == 128, "TriRec layout");
 // do not depend on the pixel (MainState.cpp:300-327, glm pairwise dot).
 // `fast` (1 or 0): every lane that can hit gets an r2 - dist2 in
 // {0} u [2^-94, 2^102], where sqrt_rn_normal equals sqrtf (see prep_sphere).
+// `tmin_key`: order_key of a lower bound of every lane's t0 (see prep_sphere;
+// 0 = no bound), for depth culling in the trace.
 struct alignas(16) SphRec {
     float cx, cy, kzw, tca2;  // kzw = Lz*Lz + Lw*Lw, tca2 = tca*tca
-    float r2, tca, fast, pad1;
+    float r2, tca, fast;
+    unsigned tmin_key;
 };
 static_assert(sizeof(SphRec) == 32, "SphRec layout");
 
@@ -127,6 +130,14 @@ struct Box { int x0, y0, x1, y1; };  // inclusive pixel range, empty if x0 > x1
 // rectangle, so empty primitives can never reach a bin or a wave tile.
 __host__ __device__ inline Box empty_box() {
     return Box{1 << 30, 1 << 30, -(1 << 30), -(1 << 30)};
+}
+
+// Unsigned key with the order of the float (for non-NaN values): positives
+// above negatives, -0 just below +0.
+__host__ __device__ inline unsigned order_key(float f) {
+    unsigned b;
+    memcpy(&b, &f, sizeof b);
+    return b ^ ((b >> 31) ? 0xffffffffu : 0x80000000u);
 }
 
 __host__ __device__ inline bool finite3(double a, double b, double c) {
@@ -271,7 +282,17 @@ __host__ __device__ inline void prep_sphere(const float* o, float radius, float 
     // dist2 >= -2^101, so r2 - dist2 <= 2^102 (and tca2 finite).
     rec->fast = (r2 >= 0x1p-70f && r2 <= 0x1p100f && fabsf(tca2) <= 0x1p100f &&
                  fabsf(kzw) <= 0x1p100f) ? 1.0f : 0.0f;
-    rec->pad1 = 0.0f;
+    // Lower bound of t0 over all pixels, by monotonicity of IEEE rounding:
+    // lx*lx + ly*ly >= 0, so dist2 = ((.) + kzw) - tca2 >= kzw - tca2 = d0,
+    // arg = r2 - dist2 <= r2 - d0 = a0, thc <= sqrtf(a0) (correctly rounded
+    // on both sides), t0 = tca - thc >= tca - sqrtf(a0).  The same float ops
+    // in the same order, so the bound holds for the computed values.
+    {
+        const float d0 = kzw - tca2;
+        const float a0 = r2 - d0;
+        const float tmin = tca - sqrtf(a0);
+        rec->tmin_key = tmin == tmin ? order_key(tmin) : 0u;  // NaN: no bound
+    }
     (void)dx;
     (void)dy;
     if (*nonfinite || !(tca >= 0.0f)) return;  // tca < 0 (or NaN): never a hit
@@ -848,6 +869,27 @@ __global__ void __launch_bounds__(64) coarse3_kernel(
 #define RT_TRACE_ATTR
 #endif
 
+#ifndef RT_DEPTH_CULL
+#define RT_DEPTH_CULL 1  // skip spheres that cannot beat any lane's closest
+#endif
+
+// Wave-uniform order_key of the largest closest[] of the wave: per-lane max
+// over its rows, then a DPP max to lane 63 (row_shr 1/2/4/8 within rows of
+// 16, row_bcast 15/31 across them; shifted-in lanes read 0, the identity).
+__device__ __forceinline__ unsigned wave_max_key(const float* closest) {
+    float m = closest[0];
+#pragma unroll
+    for (int j = 1; j < kRowsPerLane; ++j) m = fmaxf(m, closest[j]);
+    unsigned v = order_key(m);
+    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false));
+    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false));
+    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false));
+    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false));
+    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false));
+    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false));
+    return (unsigned)__builtin_amdgcn_readlane((int)v, 63);
+}
+
 // One wave per kWaveTile x kWaveTileH tile, all candidate data on scalar
 // loads: count, then ids and tile words 8 at a time, then the records of
 // the candidates this tile keeps (in the reference's primitive order).
@@ -926,6 +968,11 @@ __global__ void __launch_bounds__(64 * kTraceWaves) RT_TRACE_ATTR trace3_kernel(
     const double px = (double)x;
     const float pxf = (float)x;
 
+#if RT_DEPTH_CULL
+    // order_key of the largest `closest` in the tile, refreshed lazily
+    unsigned tile_max_key = order_key(kFar);
+    bool dirty = false;
+#endif
     const int count = kMode == 1 ? 0 : counts[cb];
     const int* __restrict__ ids = lists + (int64_t)cb * 2 * half_cap;
     const int* __restrict__ tms = ids + half_cap;
@@ -956,8 +1003,19 @@ __global__ void __launch_bounds__(64 * kTraceWaves) RT_TRACE_ATTR trace3_kernel(
                 test_tri(r, p / 12, (bits & 2u) != 0u, px, py, closest, hit);
             } else {
                 const SphRec r = sph[p - n_tri];
+#if RT_DEPTH_CULL
+                // t0 >= tmin >= every closest: no lane can take it (strict <)
+                if (dirty) {
+                    tile_max_key = wave_max_key(closest);
+                    dirty = false;
+                }
+                if (r.tmin_key >= tile_max_key) continue;
+#endif
                 test_sph(r, scene.n_cubes + (p - n_tri), pxf, pyf, closest, hit);
             }
+#if RT_DEPTH_CULL
+            dirty = true;
+#endif
         }
     }
     const bool full = rel_x + kWaveTile <= width && tile_y + kWaveTileH <= row_end;

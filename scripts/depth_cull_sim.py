@@ -1,13 +1,15 @@
 # Estimate of the depth-culling payoff on the bench scene (see DESIGN.md §3,
 # rejected variants): counts (primitive, 8x32 tile) pairs with a hit, and
 # those left after skipping primitives whose t lower bound is not below the
-# tile's current max best-t.  Host-only numpy; usage: depth_cull_sim.py [W] [seed]
+# tile's current max best-t.  Host-only numpy; usage: depth_cull_sim.py [W] [seed] [spheres] [cubes] [k]
 import sys, numpy as np, importlib
 sys.path.insert(0, str(__import__("pathlib").Path(__file__).resolve().parents[1]))
 pkg = importlib.import_module("opencl-ray-tracer_amd")
 W = H = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
-NS, NC = 256, 64
-sc = pkg.Scene.synthetic(W, H, NS, NC, seed=int(sys.argv[2]) if len(sys.argv) > 2 else 7, k=W / 640)
+NS = int(sys.argv[3]) if len(sys.argv) > 3 else 256
+NC = int(sys.argv[4]) if len(sys.argv) > 4 else 64
+K = float(sys.argv[5]) if len(sys.argv) > 5 else W / 640
+sc = pkg.Scene.synthetic(W, H, NS, NC, seed=int(sys.argv[2]) if len(sys.argv) > 2 else 7, k=K)
 TW, TH = 8, 32
 best = np.full((H, W), 300000.0, np.float32)
 prims = []

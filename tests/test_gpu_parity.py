@@ -161,6 +161,17 @@ EDGE_CASES = {
     # sphere origin w != 1 and a zero radius
     "odd_w": dict(spheres=[((50, 40, -50, 3), 20, (1, .3, .3, 255)),
                            ((20, 20, -50, 1), 0, (1, 1, 1, 255))]),
+    # depth culling: a big front sphere, layers behind it (culled once the
+    # tile is covered), spheres whose lower bound equals the front depth,
+    # a later nearer one that must still win, t0 == 0 and t < 0 spheres
+    "depth_layers": dict(spheres=[((50, 40, -30, 1), 60, (1, .2, .2, 255))] +
+                         [((45 + 3 * i, 35 + 2 * i, -30 - i, 1), 20 + i, (.2, 1, .2, 255))
+                          for i in range(12)] +
+                         [((50, 40, -30, 1), 60, (0, 0, 1, 255)),
+                          ((50, 40, -90, 1), 60, (0, 1, 1, 255)),
+                          ((30, 30, -95, 1), 90, (1, 1, 0, 255)),
+                          ((60, 50, -10, 1), 10, (1, 0, 1, 255)),
+                          ((20, 60, -4, 1), 4, (.5, .5, .5, 255))]),
 }
 
 
