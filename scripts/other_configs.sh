@@ -16,4 +16,13 @@ run --width 8192 --height 8192 --spheres 192 --cubes 64                # config 
 run --width 16384 --height 16384 --spheres 4096 --cubes 0              # config 5, whole frame, dense
 run --width 16384 --height 16384 --spheres 4096 --cubes 0 --k 1        # config 5, sparse
 run --width 4096 --height 4096 --spheres 256 --cubes 64 --format rgba8 # config 3, Texture format
+# 8-GPU configs: rank 0's band (weak-scaling layout of bench_variants.py --ranks 8)
+L=opencl-ray-tracer_amd/librt_hip.so
+band() {
+  timeout -k 10 300 python scripts/bench_variants.py $L --rounds 5 "$@" > gpurun_out/band.json 2>>gpurun_out/other_configs.err
+  rc=$?; echo "band $* rc=$rc"; [ $rc -ne 0 ] && exit $rc
+  python -c "import json,sys; d=json.load(open('gpurun_out/band.json')); print(json.dumps({'band_of_8': sys.argv[1:], 'us_per_frame': list(d.values())[0]['median_us']}))" "$@" >> $OUT
+}
+band --width 8192 --height 1024 --spheres 24 --cubes 8 --ranks 8 --k 12.8      # config 4: 8192^2 over 8 ranks
+band --width 16384 --height 2048 --spheres 512 --cubes 0 --ranks 8 --k 25.6    # config 5: 16384^2 over 8 ranks
 echo done
