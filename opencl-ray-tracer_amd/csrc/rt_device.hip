@@ -869,6 +869,9 @@ __global__ void __launch_bounds__(64) coarse3_kernel(
 #define RT_TRACE_ATTR
 #endif
 
+#ifndef RT_XCD_REMAP
+#define RT_XCD_REMAP 0  // trace: contiguous tile runs per XCD (T1 swizzle)
+#endif
 #ifndef RT_DEPTH_CULL
 #define RT_DEPTH_CULL 1  // skip spheres that cannot beat any lane's closest
 #endif
@@ -915,10 +918,23 @@ __global__ void __launch_bounds__(64 * kTraceWaves) RT_TRACE_ATTR trace3_kernel(
     // one CU: the candidate records one wave loads are scalar-cache hits for
     // the others)
     constexpr int kGroups = (kTilesX * kTilesY) / (kTraceWaves * kTilesPerWave);
-    const int cb = blockIdx.x / kGroups;
+#if RT_XCD_REMAP
+    // Workgroups are dealt round-robin over the 8 XCDs: give each XCD label
+    // (b % 8) a contiguous run of tiles, so the 16 tiles of a coarse bin
+    // share one L2 for its list and records (bijective for any grid size,
+    // cdna_hip_programming.md T1).
+    const int bid = [] {
+        const int b = (int)blockIdx.x, nwg = (int)gridDim.x;
+        const int q = nwg / 8, r = nwg % 8, xcd = b % 8;
+        return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + b / 8;
+    }();
+#else
+    const int bid = (int)blockIdx.x;
+#endif
+    const int cb = bid / kGroups;
     // wave-uniform by construction; readfirstlane tells the compiler, so the
     // per-candidate keep / inside bits stay in SGPRs (scalar branches)
-    const int wave_id = (blockIdx.x % kGroups) * kTraceWaves +
+    const int wave_id = (bid % kGroups) * kTraceWaves +
                         __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
 #if RT_TIMELINE
     const int tile = blockIdx.x * kTraceWaves + (int)(threadIdx.x >> 6);
