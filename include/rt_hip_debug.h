@@ -34,8 +34,14 @@ int rt_debug_sphere_box(const float origin[4], float radius,
                         const float dir[4], int32_t width, int32_t row_begin,
                         int32_t row_end, int32_t box_out[4], float cls_out[8]);
 
-/* Pixel shape of the tile one wave classifies and traces (w x h). */
+/* Pixel shape of the tile one wave traces (w x h). */
 int rt_debug_tile_shape(int32_t* w, int32_t* h);
+
+/* Pixel shape of the row block the coarse kernel classifies (w x h): a tile
+ * is h_tile / h blocks stacked vertically, block j holding lane row j of
+ * every lane, so each block's verdict (skip / test / u,v inside) is
+ * wave-uniform for that row. */
+int rt_debug_block_shape(int32_t* w, int32_t* h);
 
 /* Trace-kernel ablation for measurements: 0 = the real kernel, 1 = stores
  * only, 2 = no per-pixel tests, 3 = no stores.  Modes 1-3 produce wrong
@@ -43,7 +49,8 @@ int rt_debug_tile_shape(int32_t* w, int32_t* h);
 int rt_debug_set_trace_mode(rt_ctx* ctx, int mode);
 
 /* Byte budget for the coarse candidate lists (8 B x (primitives + 16) per
- * 64x64 bin); binned frames over it render as internal row bands.
+ * 64x64 bin: an id and a tile word; 20 B with RT_ROWBITS=1); binned frames
+ * over it render as internal row bands.
  * 0 restores the default (4 GiB). */
 int rt_debug_set_list_budget(rt_ctx* ctx, int64_t bytes);
 

@@ -75,6 +75,26 @@ static_assert(kCoarseW % kWaveTile == 0 && kCoarseH % kWaveTileH == 0,
 // kTileSpan pixels on any side
 constexpr int kTileSpan = kWaveTile > kWaveTileH ? kWaveTile : kWaveTileH;
 static_assert(kTileSpan <= 64, "tile span");
+// Row blocks: the classifier's unit inside a wave tile.  Lane row j of a
+// tile covers pixel rows tile_y + kLaneRows * j + [0, kLaneRows), i.e. one
+// kWaveTile x kLaneRows block per j, so a per-block verdict (skip / test /
+// u,v proven inside) is wave-uniform for each of a lane's rows.
+// RT_ROWBITS 0 (default) classifies whole tiles (one block of kWaveTileH
+// rows); 1 also classifies the row blocks of a triangle's partial tiles
+// (measured slower: the trace saves 1.1 us, coarse pays 3.7 us).
+#ifndef RT_ROWBITS
+#define RT_ROWBITS 0
+#endif
+constexpr int kBlocks = RT_ROWBITS ? kRowsPerLane : 1;   // blocks per wave tile
+constexpr int kBlockH = kWaveTileH / kBlocks;             // rows per block
+constexpr int kTileBits = 2 * kBlocks;                    // bit 2b keep, 2b+1 inside
+constexpr int kTilesPerWord = 32 / kTileBits;
+constexpr unsigned kTileMask = kTileBits == 32 ? ~0u : (1u << kTileBits) - 1u;
+constexpr unsigned kKeepMask = 0x55555555u & kTileMask;
+static_assert(kBlockH * kBlocks == kWaveTileH && kTileBits <= 32, "row blocks");
+// the block of lane row j
+__host__ __device__ constexpr int row_block(int j) { return j * kBlocks / kRowsPerLane; }
+
 constexpr int kThreads = 256;       // generic_kernel block
 constexpr int kPrepThreads = 64;  // prep: one wave per block, spread over CUs
 #ifndef RT_COMPACT
@@ -573,7 +593,7 @@ __device__ __forceinline__ unsigned rt_now() { return (unsigned)__builtin_amdgcn
 #define RT_ROWSKIP 0  // 1: skip triangle rows, 2: sphere rows, 3: both (no lane can hit)
 #endif
 
-__device__ __forceinline__ void test_tri(const TriRec& r, int slot, bool inside, double px,
+__device__ __forceinline__ void test_tri(const TriRec& r, int slot, unsigned bits, double px,
                                          const double* py, float* closest, int* hit) {
     const double tx = px - r.v0x;
     const double txe1y = tx * r.e1y;               // q2 = tx*e1y - ty*e1x
@@ -582,10 +602,13 @@ __device__ __forceinline__ void test_tri(const TriRec& r, int slot, bool inside,
     const double txp0 = tx * r.p0;                 // u = (tx*p0 + ty*p1) * inv_det
 #pragma unroll
     for (int j = 0; j < kRowsPerLane; ++j) {
+        // this row's block: bit 0 keep, bit 1 u,v proven inside (wave-uniform)
+        const unsigned rb = bits >> (2 * row_block(j));
+        if (!(rb & 1u)) continue;
         const double ty = py[j] - r.v0y;
         const double q2 = txe1y - ty * r.e1x;
         bool pass = true;
-        if (!inside) {  // wave-uniform
+        if (!(rb & 2u)) {
             const double u = (txp0 + ty * r.p1) * r.inv_det;
             const double v = (r.dz * q2) * r.inv_det;
             pass = !((u < 0.0) | (u > 1.0) | (v < 0.0) | (u + v > 1.0));
@@ -615,8 +638,8 @@ __device__ __forceinline__ float sqrt_rn_normal(float x) {
     return r;
 }
 
-__device__ __forceinline__ void test_sph(const SphRec& s, int slot, float pxf, const float* pyf,
-                                         float* closest, int* hit) {
+__device__ __forceinline__ void test_sph(const SphRec& s, int slot, unsigned bits, float pxf,
+                                         const float* pyf, float* closest, int* hit) {
     const float lx = s.cx - pxf;
     const float lx2 = lx * lx;
     float dist2[kRowsPerLane], arg[kRowsPerLane];
@@ -632,6 +655,7 @@ __device__ __forceinline__ void test_sph(const SphRec& s, int slot, float pxf, c
     const bool general = !(s.fast != 0.0f);
 #pragma unroll
     for (int j = 0; j < kRowsPerLane; ++j) {
+        if (!((bits >> (2 * row_block(j))) & 1u)) continue;  // block skipped (uniform)
         // no lane of this row within the sphere's disc: nothing to update
         if ((RT_ROWSKIP & 2) && __ballot(!(dist2[j] > s.r2)) == 0ull) continue;
         const float thc = general ? sqrtf(arg[j]) : sqrt_rn_normal(arg[j]);
@@ -642,11 +666,12 @@ __device__ __forceinline__ void test_sph(const SphRec& s, int slot, float pxf, c
     }
 }
 
-// Tile classification of one candidate against the wave tile
-// [x0, x0+kWaveTile-1] x [y0, y0+kWaveTileH-1] (fp32, conservative; see Cls).
+// Tile classification of one candidate against the rectangle
+// [x0, x0+kW-1] x [y0, y0+kH-1] (fp32, conservative; see Cls).
+template <int kWpx = kWaveTile, int kHpx = kWaveTileH>
 __device__ __forceinline__ void classify(const Cls& k, bool is_tri, float x0, float y0,
                                          bool* keep, bool* inside) {
-    constexpr float kW = (float)(kWaveTile - 1), kH = (float)(kWaveTileH - 1);
+    constexpr float kW = (float)(kWpx - 1), kH = (float)(kHpx - 1);
     if (is_tri) {
         const float xl = x0 - k.a.x, xh = (x0 + kW) - k.a.x;
         const float yl = y0 - k.a.y, yh = (y0 + kH) - k.a.y;
@@ -740,16 +765,22 @@ __device__ __forceinline__ void shade_store(const float4* __restrict__ colours,
 // Tiles of one coarse bin: kCoarseW / kWaveTile x kCoarseH / kWaveTileH.
 constexpr int kTilesX = kCoarseW / kWaveTile;
 constexpr int kTilesY = kCoarseH / kWaveTileH;
-static_assert(kTilesX * kTilesY <= 16, "two bits per tile in one 32-bit word");
+constexpr int kTiles = kTilesX * kTilesY;
+// tile words per candidate: kTileBits per tile, kTilesPerWord tiles a word
+constexpr int kTmWords = (kTiles + kTilesPerWord - 1) / kTilesPerWord;
+// ints per candidate slot of a coarse-bin list: the id, then the tile words
+constexpr int kListStride = 1 + kTmWords;
+static_assert(kTiles <= 16 && kTmWords <= 4, "tile words");
 
-// Coarse binning with per-tile classification: one wave per coarse bin.
+// Coarse binning with per-block classification: one wave per coarse bin.
 // (1) the ids whose box touches the coarse bin are compacted, in primitive
 // order, into LDS (rounds of kRound); (2) the (candidate, tile) pairs are
 // spread over the lanes, 16 lanes per candidate, each testing box overlap +
-// tile classifier and OR-ing its two bits (bit 2t keep, bit 2t+1 inside)
-// into the candidate's LDS word; (3) candidates kept by some tile are
-// appended in order.  Output: counts[cb]; ids at lists[cb * 2 * half_cap
-// ...] and tile words at lists[cb * 2 * half_cap + half_cap ...].
+// classifier for every row block of its tile and OR-ing the bits (per
+// block b: bit 2b keep, bit 2b+1 inside) into the candidate's LDS tile word;
+// (3) candidates kept by some block are appended in order.  Output:
+// counts[cb]; at lists + cb * kListStride * half_cap: half_cap ids, then
+// tile word w of every candidate at [(1 + w) * half_cap ...].
 #ifndef RT_C3_ABL
 #define RT_C3_ABL 0  // diagnostics only: 1 = box scan + compaction, nothing classified or listed;
                      // 2 = as 1, every wave reading the same 64 boxes (L1-resident)
@@ -766,14 +797,14 @@ __global__ void __launch_bounds__(64) coarse3_kernel(
     int n_cx, const int* __restrict__ live_ids, const int* __restrict__ n_live, int row_begin,
     int half_cap, int* __restrict__ counts, int* __restrict__ lists) {
     __shared__ int s_ids[kRound];
-    __shared__ unsigned s_tm[kRound];
+    __shared__ unsigned s_tm[kRound * kTmWords];
     __shared__ int4 s_box[kRound];
     __shared__ Cls s_cls[kRound];
     const int cb = blockIdx.x;
     const int lane = threadIdx.x;
     const int x0 = (cb % n_cx) * kCoarseW, x1 = x0 + kCoarseW - 1;
     const int y0 = row_begin + (cb / n_cx) * kCoarseH, y1 = y0 + kCoarseH - 1;
-    int* out_id = lists + (int64_t)cb * 2 * half_cap;
+    int* out_id = lists + (int64_t)cb * kListStride * half_cap;
     int* out_tm = out_id + half_cap;
     int count = 0;   // appended to the output
     int staged = 0;  // ids in s_ids
@@ -784,41 +815,64 @@ __global__ void __launch_bounds__(64) coarse3_kernel(
         // each candidate's box and classifier into LDS once
         for (int e = lane; e < n; e += 64) {
             const int id = s_ids[e];
-            s_tm[e] = 0u;
+#pragma unroll
+            for (int w = 0; w < kTmWords; ++w) s_tm[e * kTmWords + w] = 0u;
             s_box[e] = boxes[id];
             s_cls[e] = cls[id];
         }
         __builtin_amdgcn_wave_barrier();
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        constexpr int kTiles = kTilesX * kTilesY;
         for (int q0 = 0; q0 < n * kTiles; q0 += 64) {
             const int q = q0 + lane;
             if (q < n * kTiles) {
                 const int c = q / kTiles, t = q % kTiles;
-                const int id = s_ids[c];
+                const bool is_tri = s_ids[c] < n_tri;
                 const int4 pb = s_box[c];
                 const int tx = x0 + (t % kTilesX) * kWaveTile;
                 const int ty = y0 + (t / kTilesX) * kWaveTileH;
+                unsigned bits = 0u;
                 bool keep = false, inside = false;
                 if (pb.x <= tx + kWaveTile - 1 && pb.z >= tx && pb.y <= ty + kWaveTileH - 1 &&
                     pb.w >= ty)
-                    classify(s_cls[c], id < n_tri, (float)tx, (float)ty, &keep, &inside);
-                const unsigned bits = (keep ? 1u : 0u) | (keep && inside ? 2u : 0u);
-                if (bits) atomicOr(&s_tm[c], bits << (2 * t));
+                    classify(s_cls[c], is_tri, (float)tx, (float)ty, &keep, &inside);
+                if (keep) bits = inside ? kTileMask : kKeepMask;
+#if RT_ROWBITS == 1
+                // a triangle's partial tile: classify each row block
+                if (kBlocks > 1 && is_tri && keep && !inside) {
+                    bits = 0u;
+#pragma unroll
+                    for (int b = 0; b < kBlocks; ++b) {
+                        const int by = ty + b * kBlockH;
+                        bool bk = false, bi = false;
+                        if (pb.y <= by + kBlockH - 1 && pb.w >= by)
+                            classify<kWaveTile, kBlockH>(s_cls[c], true, (float)tx, (float)by, &bk, &bi);
+                        bits |= ((bk ? 1u : 0u) | (bk && bi ? 2u : 0u)) << (2 * b);
+                    }
+                }
+#endif
+                if (bits)
+                    atomicOr(&s_tm[c * kTmWords + t / kTilesPerWord],
+                             bits << (kTileBits * (t % kTilesPerWord)));
             }
         }
         __builtin_amdgcn_wave_barrier();
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
         for (int e0 = 0; e0 < n; e0 += 64) {
             const int e = e0 + lane;
-            const unsigned tm = e < n ? s_tm[e] : 0u;
-            const bool any = tm != 0u;
+            unsigned tm[kTmWords];
+            bool any = false;
+#pragma unroll
+            for (int w = 0; w < kTmWords; ++w) {
+                tm[w] = e < n ? s_tm[e * kTmWords + w] : 0u;
+                any |= tm[w] != 0u;
+            }
             const unsigned long long m2 = __ballot(any);
             if (any) {
-                const unsigned below = __builtin_amdgcn_mbcnt_hi(
+                const int pos = count + (int)__builtin_amdgcn_mbcnt_hi(
                     (unsigned)(m2 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m2, 0u));
-                out_id[count + (int)below] = s_ids[e];
-                out_tm[count + (int)below] = (int)tm;
+                out_id[pos] = s_ids[e];
+#pragma unroll
+                for (int w = 0; w < kTmWords; ++w) out_tm[w * half_cap + pos] = (int)tm[w];
             }
             count += __popcll(m2);
         }
@@ -990,8 +1044,9 @@ __global__ void __launch_bounds__(64 * kTraceWaves) RT_TRACE_ATTR trace3_kernel(
     bool dirty = false;
 #endif
     const int count = kMode == 1 ? 0 : counts[cb];
-    const int* __restrict__ ids = lists + (int64_t)cb * 2 * half_cap;
-    const int* __restrict__ tms = ids + half_cap;
+    const int* __restrict__ ids = lists + (int64_t)cb * kListStride * half_cap;
+    const int* __restrict__ tms = ids + (1 + t / kTilesPerWord) * half_cap;  // this tile's word
+    const int tm_shift = kTileBits * (t % kTilesPerWord);
 #if RT_TIMELINE
     tl1 = rt_now();
 #endif
@@ -1006,8 +1061,8 @@ __global__ void __launch_bounds__(64 * kTraceWaves) RT_TRACE_ATTR trace3_kernel(
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             if (k >= n) break;
-            const unsigned bits = ((unsigned)tmv[k] >> (2 * t)) & 3u;
-            if (!(bits & 1u)) continue;
+            const unsigned bits = ((unsigned)tmv[k] >> tm_shift) & kTileMask;
+            if (!(bits & kKeepMask)) continue;
             const int p = idv[k];
             if (kMode == 2) {
                 hit[0] = hit[0] > p ? hit[0] : -1;
@@ -1016,7 +1071,7 @@ __global__ void __launch_bounds__(64 * kTraceWaves) RT_TRACE_ATTR trace3_kernel(
             if (p < n_tri) {
                 const TriRec r = tri[p];
                 asm volatile("" ::"s"(r.p0), "s"(r.p1), "s"(r.dz));
-                test_tri(r, p / 12, (bits & 2u) != 0u, px, py, closest, hit);
+                test_tri(r, p / 12, bits, px, py, closest, hit);
             } else {
                 const SphRec r = sph[p - n_tri];
 #if RT_DEPTH_CULL
@@ -1027,7 +1082,7 @@ __global__ void __launch_bounds__(64 * kTraceWaves) RT_TRACE_ATTR trace3_kernel(
                 }
                 if (r.tmin_key >= tile_max_key) continue;
 #endif
-                test_sph(r, scene.n_cubes + (p - n_tri), pxf, pyf, closest, hit);
+                test_sph(r, scene.n_cubes + (p - n_tri), bits, pxf, pyf, closest, hit);
             }
 #if RT_DEPTH_CULL
             dirty = true;
@@ -1080,7 +1135,7 @@ struct rt_ctx {
     unsigned* flag = nullptr;   // non-finite scene flag (generation-stamped)
     unsigned gen = 0;
     int trace_mode = 0;  // diagnostics ablation, see trace3_kernel
-    // coarse lists take 8 B x (primitives + 16) per 64x64 bin; a frame whose
+    // coarse lists take 4 B x kListStride x (primitives + 16) per 64x64 bin; a frame whose
     // lists would exceed this is rendered as internal row bands
     int64_t list_budget = (int64_t)4 << 30;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -1177,7 +1232,8 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
         // coarse rows, each a band render (prep compacts to its primitives),
         // in order on the same stream.
         const int64_t n_prims = 12 * (int64_t)s->num_cubes + s->num_spheres;
-        const int64_t row_bytes = 8 * ((n_prims + 7) / 8 * 8 + 8) * ((width + kCoarseW - 1) / kCoarseW);
+        const int64_t row_bytes =
+            4 * kListStride * ((n_prims + 7) / 8 * 8 + 8) * ((width + kCoarseW - 1) / kCoarseW);
         const int64_t n_cy = (rows + kCoarseH - 1) / kCoarseH;
         if (n_cy > 1 && row_bytes * n_cy > ctx->list_budget) {
             const int64_t per = std::max<int64_t>(1, ctx->list_budget / row_bytes) * kCoarseH;
@@ -1226,7 +1282,7 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
     // one trace work-item per 64 x kTraceWaves; AQL grid sizes are 32-bit
     if (n_wgs * 64 * kTraceWaves > (int64_t)UINT32_MAX) return RT_ERR_INVALID_ARG;
     const int n_coarse = (int)n_coarse64;
-    // per coarse bin: candidate ids, then their tile words (half_cap each,
+    // per coarse bin: candidate ids, then each tile word (half_cap each,
     // padded by 8 so the trace's 8-wide scalar reads stay inside the bin)
     const int half_cap = (n_prims + 7) / 8 * 8 + 8;
 
@@ -1243,7 +1299,7 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
     const size_t rec_need = mask_off + align_up(sizeof(unsigned long long) * (size_t)n_chunks, 256);
     rc = ensure(&ctx->rec_buf, &ctx->rec_cap, rec_need);
     if (rc) return rc;
-    const size_t list_need = sizeof(int) * 2 * (size_t)half_cap * (size_t)n_coarse + 256;
+    const size_t list_need = sizeof(int) * kListStride * (size_t)half_cap * (size_t)n_coarse + 256;
     rc = ensure(&ctx->list_buf, &ctx->list_cap, list_need);
     if (rc) return rc;
     char* base = static_cast<char*>(ctx->rec_buf);
@@ -1551,6 +1607,13 @@ int rt_debug_tile_shape(int32_t* w, int32_t* h) {
     if (!w || !h) return RT_ERR_INVALID_ARG;
     *w = kWaveTile;
     *h = kWaveTileH;
+    return RT_OK;
+}
+
+int rt_debug_block_shape(int32_t* w, int32_t* h) {
+    if (!w || !h) return RT_ERR_INVALID_ARG;
+    *w = kWaveTile;
+    *h = kBlockH;
     return RT_OK;
 }
 

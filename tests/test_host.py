@@ -69,6 +69,21 @@ def tile_shape(pkg):
     return w.value, h.value
 
 
+def block_shape(pkg):
+    w, h = ctypes.c_int32(), ctypes.c_int32()
+    assert pkg.library().rt_debug_block_shape(ctypes.byref(w), ctypes.byref(h)) == 0
+    return w.value, h.value
+
+
+def classified_shapes(pkg):
+    """The rectangles the coarse kernel classifies: row blocks (and whole
+    tiles, which the tests keep checking as a stronger property)."""
+    tw, th = tile_shape(pkg)
+    bw, bh = block_shape(pkg)
+    assert bw == tw and th % bh == 0
+    return sorted({(tw, th), (bw, bh)})
+
+
 def classify_tile(cls, is_tri, x0, y0, tw, th):
     """numpy float32 mirror of the trace kernel's classify() (rt_device.hip)
     on a tw x th wave tile."""
@@ -140,6 +155,7 @@ def test_triangle_box_and_tile_classifier_are_conservative(pkg, oracle, band):
     w, h = 176, 160
     rb, re = band
     tw, th = tile_shape(pkg)
+    shapes = classified_shapes(pkg)
     rng = np.random.default_rng(7 + rb)
     n_inside_tiles = n_skip_tiles = 0
     for v in random_triangles(rng, w, h, 150):
@@ -161,24 +177,25 @@ def test_triangle_box_and_tile_classifier_are_conservative(pkg, oracle, band):
             sub = hits[y0 - rb:y1 - rb + 1, x0:x1 + 1].astype(bool)
             assert not (out_px & sub).any(), v
             assert not (in_px & ~sub).any(), v
-        for ty in range(rb, re, th):
-            for tx in range(0, w, tw):
-                if box[0] > tx + tw - 1 or box[2] < tx or box[1] > ty + th - 1 or box[3] < ty:
-                    continue  # the kernel classifies only tiles the box touches
-                keep, inside = classify_tile(cls, True, tx, ty, tw, th)
-                tile = hits[ty - rb:ty - rb + th, tx:tx + tw]
-                if not keep:
-                    n_skip_tiles += 1
-                    assert not tile.any(), (v, tx, ty)
-                if inside:
-                    n_inside_tiles += 1
-                    assert tile.all(), (v, tx, ty)
+        for sw, sh in shapes:
+            for ty in range(rb, re, sh):
+                for tx in range(0, w, sw):
+                    if box[0] > tx + sw - 1 or box[2] < tx or box[1] > ty + sh - 1 or box[3] < ty:
+                        continue  # the kernel classifies only rectangles the box touches
+                    keep, inside = classify_tile(cls, True, tx, ty, sw, sh)
+                    tile = hits[ty - rb:ty - rb + sh, tx:tx + sw]
+                    if not keep:
+                        n_skip_tiles += 1
+                        assert not tile.any(), (v, tx, ty, sw, sh)
+                    if inside:
+                        n_inside_tiles += 1
+                        assert tile.all(), (v, tx, ty, sw, sh)
     assert n_inside_tiles > 0 and n_skip_tiles > 0  # the classifier does something
 
 
 def test_sphere_box_and_tile_classifier_are_conservative(pkg, oracle):
     w, h = 160, 128
-    tw, th = tile_shape(pkg)
+    shapes = classified_shapes(pkg)
     rng = np.random.default_rng(11)
     for i in range(120):
         c = np.float32([rng.uniform(-30, w + 30), rng.uniform(-30, h + 30),
@@ -193,11 +210,12 @@ def test_sphere_box_and_tile_classifier_are_conservative(pkg, oracle):
             assert box[1] <= ys.min() and ys.max() <= box[3]
         elif box[0] > box[2]:
             continue
-        for ty in range(0, h, th):
-            for tx in range(0, w, tw):
-                keep, _ = classify_tile(cls, False, tx, ty, tw, th)
-                if not keep:
-                    assert not hits[ty:ty + th, tx:tx + tw].any(), (c, r, tx, ty)
+        for tw, th in shapes:
+            for ty in range(0, h, th):
+                for tx in range(0, w, tw):
+                    keep, _ = classify_tile(cls, False, tx, ty, tw, th)
+                    if not keep:
+                        assert not hits[ty:ty + th, tx:tx + tw].any(), (c, r, tx, ty, tw, th)
 
 
 def _decode_png(path):
