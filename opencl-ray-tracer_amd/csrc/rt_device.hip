@@ -51,9 +51,6 @@ namespace {
 #ifndef RT_TRACE_WAVES
 #define RT_TRACE_WAVES 8          // amdgpu_waves_per_eu floor for trace (0 = none)
 #endif
-#ifndef RT_NT_STORE
-#define RT_NT_STORE 0             // nontemporal frame stores
-#endif
 #ifndef RT_TIMELINE
 #define RT_TIMELINE 0             // diagnostics: per-wave phase timestamps
 #endif
@@ -693,23 +690,6 @@ __device__ __forceinline__ void classify(const Cls& k, bool is_tri, float x0, fl
     }
 }
 
-__device__ __forceinline__ void store_pixel(void* __restrict__ out, int out_format, int64_t idx,
-                                            int4v pix) {
-#if RT_NT_STORE
-    // streaming stores: the frame is written once and never re-read here
-    if (out_format == RT_FORMAT_I32X4)
-        __builtin_nontemporal_store(pix, reinterpret_cast<int4v*>(out) + idx);
-    else
-        __builtin_nontemporal_store(pack_rgba8(pix), reinterpret_cast<unsigned*>(out) + idx);
-#else
-    if (out_format == RT_FORMAT_I32X4)
-        reinterpret_cast<int4v*>(out)[idx] = pix;
-    else
-        reinterpret_cast<unsigned*>(out)[idx] = pack_rgba8(pix);
-#endif
-}
-
-// Shade (MainState.cpp:396-407) and store one lane's kRowsPerLane pixels.
 // Pixel value of the Texture format (MainState.cpp:1026-1036) or int32x4.
 template <int kFmt>
 __device__ __forceinline__ void store_fmt(void* __restrict__ out, int64_t idx, int4v pix) {
@@ -719,19 +699,13 @@ __device__ __forceinline__ void store_fmt(void* __restrict__ out, int64_t idx, i
         reinterpret_cast<unsigned*>(out)[idx] = pack_rgba8(pix);
 }
 
-// Shade (MainState.cpp:396-407) and store one lane's kRowsPerLane pixels
-// (rows kLaneRows apart).  `full`: the whole wave tile lies inside the frame
-// band, so no per-lane bounds checks.
-template <int kMode, int kFmt>
-__device__ __forceinline__ void shade_store(const float4* __restrict__ colours,
-                                            const float* closest, const int* hit, int x, int y0,
-                                            int width, int row_begin, int row_end, bool full,
-                                            void* __restrict__ out) {
+// Shade (MainState.cpp:396-407) one lane's kRowsPerLane pixels.
+__device__ __forceinline__ void shade_pixels(const float4* __restrict__ colours,
+                                             const float* closest, const int* hit, int4v* pix) {
     bool lane_hit = false;
 #pragma unroll
     for (int j = 0; j < kRowsPerLane; ++j) lane_hit |= hit[j] >= 0;
     const bool any_hit = __ballot(lane_hit) != 0ull;
-    int4v pix[kRowsPerLane];
 #pragma unroll
     for (int j = 0; j < kRowsPerLane; ++j) pix[j] = int4v{0, 0, 0, 255};
     if (any_hit) {
@@ -746,6 +720,16 @@ __device__ __forceinline__ void shade_store(const float4* __restrict__ colours,
             if (hit[j] >= 0) pix[j] = c;
         }
     }
+}
+
+// Store one lane's kRowsPerLane pixels (rows kLaneRows apart) of the wave
+// tile at (tile_x, tile_y), in the Texture format (MainState.cpp:1026-1036)
+// or int32x4.  `full`: the whole tile lies inside the frame band, so no
+// per-lane bounds checks.
+template <int kMode, int kFmt>
+__device__ __forceinline__ void store_rows(const int4v* pix, int x, int y0, int width,
+                                           int row_begin, int row_end, bool full,
+                                           void* __restrict__ out) {
     const int64_t idx0 = (int64_t)(y0 - row_begin) * width + x;
     const int64_t row_step = (int64_t)kLaneRows * width;
 #pragma unroll
@@ -960,6 +944,15 @@ constexpr int kTraceWaves = RT_TRACE_WG;
 constexpr int kTilesPerWave = RT_TPW;
 static_assert((kTilesX * kTilesY) % (kTraceWaves * kTilesPerWave) == 0,
               "trace workgroups must tile a coarse bin");
+// Store hand-off (RT_LDS_STORE, with RT_TRACE_WG > 1): every wave of a
+// trace workgroup leaves its shaded pixels in LDS and ends; the wave that
+// finishes last issues the whole workgroup's frame stores, so only it waits
+// for store acknowledgements at s_endpgm.  Measured slower on config 3
+// (rejected variants); off.
+#ifndef RT_LDS_STORE
+#define RT_LDS_STORE 0
+#endif
+static_assert(!RT_LDS_STORE || kTilesPerWave == 1, "store hand-off: one tile per wave");
 
 template <int kMode, int kFmt>
 __global__ void __launch_bounds__(64 * kTraceWaves) RT_TRACE_ATTR trace3_kernel(
@@ -1001,29 +994,44 @@ __global__ void __launch_bounds__(64 * kTraceWaves) RT_TRACE_ATTR trace3_kernel(
     const unsigned long long tlc0 = __builtin_amdgcn_s_memtime();
     unsigned tl1 = 0, tl2 = 0;
 #endif
+#if RT_LDS_STORE
+    __shared__ int4v s_pix[kTraceWaves][kRowsPerLane][64];
+    __shared__ int s_done;
+    if (threadIdx.x == 0) s_done = 0;
+    __syncthreads();
+#endif
 #pragma unroll 1
     for (int it = 0; it < kTilesPerWave; ++it) {
     const int t = wave_id * kTilesPerWave + it;
     const int rel_x = (cb % n_cx) * kCoarseW + (t % kTilesX) * kWaveTile;
     const int rel_y = (cb / n_cx) * kCoarseH + (t / kTilesX) * kWaveTileH;  // vs row_begin
-    if (rel_x >= width || rel_y >= row_end - row_begin) continue;  // wave-uniform
     const int tile_x = rel_x, tile_y = row_begin + rel_y;
     const int x = tile_x + (lane % kWaveTile);
     const int y0 = tile_y + (lane / kWaveTile);
+    // wave-uniform: tiles past the frame's right or bottom edge render nothing
+    const bool tile_in = rel_x < width && rel_y < row_end - row_begin;
+#if RT_LDS_STORE
+    const int w_self = (int)(threadIdx.x >> 6);
+#endif
 
-    if (kMode == 0 && *nonfinite_flag == gen) {
+    if (tile_in && kMode == 0 && *nonfinite_flag == gen) {
         // Non-finite scene data: run the reference algorithm verbatim.
 #pragma unroll 1
         for (int j = 0; j < kRowsPerLane; ++j) {
             const int y = y0 + kLaneRows * j;
-            if (x >= width || y >= row_end) continue;
-            const int4v p =
-                collide_generic(scene, make_float4((float)x, (float)y, 0.0f, 1.0f), dir);
-            store_pixel(out, out_format, (int64_t)(y - row_begin) * width + x, p);
+            int4v p = int4v{0, 0, 0, 255};
+            if (x < width && y < row_end)
+                p = collide_generic(scene, make_float4((float)x, (float)y, 0.0f, 1.0f), dir);
+#if RT_LDS_STORE
+            s_pix[w_self][j][lane] = p;
+#else
+            if (x < width && y < row_end)
+                store_fmt<kFmt>(out, (int64_t)(y - row_begin) * width + x, p);
+#endif
         }
-        continue;
-    }
-
+    } else {
+    int4v pix[kRowsPerLane];  // assigned after the walk (not live during it)
+    if (tile_in) {
     float closest[kRowsPerLane];
     int hit[kRowsPerLane];
     double py[kRowsPerLane];
@@ -1037,7 +1045,6 @@ __global__ void __launch_bounds__(64 * kTraceWaves) RT_TRACE_ATTR trace3_kernel(
     }
     const double px = (double)x;
     const float pxf = (float)x;
-
 #if RT_DEPTH_CULL
     // order_key of the largest `closest` in the tile, refreshed lazily
     unsigned tile_max_key = order_key(kFar);
@@ -1089,11 +1096,48 @@ __global__ void __launch_bounds__(64 * kTraceWaves) RT_TRACE_ATTR trace3_kernel(
 #endif
         }
     }
-    const bool full = rel_x + kWaveTile <= width && tile_y + kWaveTileH <= row_end;
 #if RT_TIMELINE
     tl2 = rt_now();
 #endif
-    shade_store<kMode, kFmt>(colours, closest, hit, x, y0, width, row_begin, row_end, full, out);
+    shade_pixels(colours, closest, hit, pix);
+    } else {  // outside the frame: nothing is stored
+#pragma unroll
+        for (int j = 0; j < kRowsPerLane; ++j) pix[j] = int4v{0, 0, 0, 255};
+    }
+#if RT_LDS_STORE
+#pragma unroll
+    for (int j = 0; j < kRowsPerLane; ++j) s_pix[w_self][j][lane] = pix[j];
+#else
+    if (tile_in) {
+        const bool full = rel_x + kWaveTile <= width && tile_y + kWaveTileH <= row_end;
+        store_rows<kMode, kFmt>(pix, x, y0, width, row_begin, row_end, full, out);
+    }
+#endif
+    }  // finite scene
+#if RT_LDS_STORE
+    // then the last wave of the workgroup stores every tile
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // every lane's deposit
+    int prev = 0;
+    if (lane == 0)
+        prev = __hip_atomic_fetch_add(&s_done, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+    prev = __builtin_amdgcn_readfirstlane(prev);
+    if (prev == kTraceWaves - 1) {  // the other waves' deposits are complete
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#pragma unroll 1
+        for (int w = 0; w < kTraceWaves; ++w) {
+            const int tw = (bid % kGroups) * kTraceWaves + w;
+            const int wx = (cb % n_cx) * kCoarseW + (tw % kTilesX) * kWaveTile;
+            const int wy = (cb / n_cx) * kCoarseH + (tw / kTilesX) * kWaveTileH;
+            if (wx >= width || wy >= row_end - row_begin) continue;  // uniform
+            int4v q[kRowsPerLane];
+#pragma unroll
+            for (int j = 0; j < kRowsPerLane; ++j) q[j] = s_pix[w][j][lane];
+            const bool full = wx + kWaveTile <= width && row_begin + wy + kWaveTileH <= row_end;
+            store_rows<kMode, kFmt>(q, wx + (lane % kWaveTile), row_begin + wy + (lane / kWaveTile),
+                                    width, row_begin, row_end, full, out);
+        }
+    }
+#endif
     }  // tiles of this wave
 #if RT_TIMELINE
     {
