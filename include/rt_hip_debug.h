@@ -54,6 +54,11 @@ int rt_debug_set_trace_mode(rt_ctx* ctx, int mode);
  * 0 restores the default (4 GiB). */
 int rt_debug_set_list_budget(rt_ctx* ctx, int64_t bytes);
 
+/* Coarse binning source: 1 (default) = the separable bin-row / bin-column
+ * masks prep publishes, 0 = scan every primitive's box (the path frames with
+ * more than 4096 bin rows + columns take). */
+int rt_debug_set_bin_masks(rt_ctx* ctx, int enable);
+
 #ifdef __cplusplus
 }
 #endif

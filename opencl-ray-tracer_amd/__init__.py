@@ -132,6 +132,7 @@ def library() -> ctypes.CDLL:
         "rt_debug_sphere_box": (ctypes.c_int, [vp, f32, vp, i32, i32, i32, vp, vp]),
         "rt_debug_set_trace_mode": (ctypes.c_int, [vp, ctypes.c_int]),
         "rt_debug_set_list_budget": (ctypes.c_int, [vp, ctypes.c_int64]),
+        "rt_debug_set_bin_masks": (ctypes.c_int, [vp, ctypes.c_int]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -387,6 +388,12 @@ class RayTracer:
         """Diagnostics: coarse-list byte budget (0 = default); frames over it
         render as internal row bands."""
         _check(library().rt_debug_set_list_budget(self._ctx, nbytes), "rt_debug_set_list_budget")
+
+    def set_bin_masks(self, enable: bool) -> None:
+        """Diagnostics: coarse binning from the separable bin masks (default)
+        or from a scan of every primitive's box."""
+        _check(library().rt_debug_set_bin_masks(self._ctx, int(bool(enable))),
+               "rt_debug_set_bin_masks")
 
     def device_info(self) -> dict:
         name = ctypes.create_string_buffer(256)

@@ -94,8 +94,15 @@ __host__ __device__ constexpr int row_block(int j) { return j * kBlocks / kRowsP
 
 constexpr int kThreads = 256;       // generic_kernel block
 constexpr int kPrepThreads = 64;  // prep: one wave per block, spread over CUs
-#ifndef RT_COMPACT
-#define RT_COMPACT 1              // band compaction: 0 never, 1 band renders, 2 always
+// Separable bin masks: a box overlaps a coarse bin iff it overlaps the bin's
+// row of bins and its column of bins, so prep publishes, per bin row and per
+// bin column, one 64-bit ballot per 64-primitive chunk, and a coarse wave
+// ANDs its row's and column's words to get its candidates in primitive
+// order without reading any box.  Frames with more than kMaskBinsMax bin
+// rows + columns (extreme aspect ratios) scan the boxes instead.
+constexpr int kMaskBinsMax = 4096;
+#ifndef RT_BIN_MASKS
+#define RT_BIN_MASKS 1            // default of rt_debug_set_bin_masks
 #endif
 constexpr double kEpsilon = 0.000001;      // MainState.cpp:15
 constexpr float kFar = 300000.0f;          // MainState.cpp:345
@@ -482,19 +489,16 @@ __global__ void __launch_bounds__(kThreads) generic_kernel(
 // ---------------------------------------------------------------------------
 // Binned path
 // ---------------------------------------------------------------------------
-// Band compaction (`live` != nullptr, band renders): the in-band primitives
-// (non-empty boxes) are listed in primitive order so that the coarse kernel
-// scans only them.  Each wave publishes a 64-bit ballot of its live lanes
-// with agent-scope (sc1) stores, drains them, and bumps `done`; the wave
-// that arrives last (no waiting anywhere) reads every chunk mask with sc1
-// loads, expands them into live_ids[], writes the count and resets `done`
-// for the next render.
+// Bin masks (`row_masks` != nullptr): after its records and boxes, each prep
+// wave (one 64-primitive chunk) writes row_masks[r * n_chunks + chunk] and
+// col_masks[c * n_chunks + chunk]: the ballot of its primitives whose box
+// overlaps bin row r / bin column c.  Every word is written every frame.
 __global__ void __launch_bounds__(kPrepThreads) prep_kernel(
     SceneDev scene, float4 dir, int width, int row_begin, int row_end,
     TriRec* __restrict__ tri, SphRec* __restrict__ sph, int4* __restrict__ boxes,
     Cls* __restrict__ cls, float4* __restrict__ colours, unsigned* __restrict__ nonfinite_flag,
-    unsigned gen, unsigned long long* chunk_masks, unsigned* done, int* __restrict__ live_ids,
-    int* __restrict__ n_live) {
+    unsigned gen, unsigned long long* __restrict__ row_masks,
+    unsigned long long* __restrict__ col_masks, int n_cx, int n_cy) {
     const int n_tri = 12 * scene.n_cubes;
     const int n_prims = n_tri + scene.n_spheres;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -526,45 +530,47 @@ __global__ void __launch_bounds__(kPrepThreads) prep_kernel(
         cls[i] = k;
         if (bad) atomicMax(nonfinite_flag, gen);
     }
-    if (!live_ids) return;
-
-    // ---- band compaction ----
-    const unsigned long long m = __ballot(i < n_prims && b.x0 <= b.x1);
-    if (lane == 0)
-        __hip_atomic_store(&chunk_masks[blockIdx.x], m, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the sc1 store has landed
-    unsigned prev = 0;
-    if (lane == 0) prev = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    prev = __shfl(prev, 0);
-    if (prev != gridDim.x - 1) return;  // not the last wave to arrive
-    // lane l expands chunk word c0 + l: wave prefix sum of the popcounts
-    // gives its output offset; the ids keep the primitive order
+    if (!row_masks) return;
+    const int chunk = (int)blockIdx.x;
     const int n_chunks = (int)gridDim.x;
-    int base = 0;
-    for (int c0 = 0; c0 < n_chunks; c0 += 64) {
-        unsigned long long mine =
-            c0 + lane < n_chunks ? __hip_atomic_load(&chunk_masks[c0 + lane], __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT)
-                                 : 0ull;
-        const int cnt = __popcll(mine);
-        int incl = cnt;  // inclusive scan over lanes
+    const bool live = i < n_prims && b.x0 <= b.x1 && b.y0 <= b.y1;
+    // Per block of 64 bins, lane r builds bin r's word without a ballot per
+    // bin: first[r] / last[r] collect the primitives whose box starts / ends
+    // in bin r (LDS OR), a prefix OR of first and a suffix OR of last (plus
+    // the primitives starting before / ending after the block) give the
+    // primitives with start <= r and end >= r; their AND is bin r's word.
+    __shared__ unsigned long long s_first[64], s_last[64];
+    auto bin_words = [&](int lo, int hi, int n_bins, int bin_px, unsigned long long* out) {
+        const int blo = live ? lo / bin_px : INT32_MAX;
+        const int bhi = live ? hi / bin_px : -1;
+        const unsigned long long me = 1ull << lane;
+        for (int r0 = 0; r0 < n_bins; r0 += 64) {
+            s_first[lane] = 0ull;
+            s_last[lane] = 0ull;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            if (blo >= r0 && blo < r0 + 64) atomicOr(&s_first[blo - r0], me);
+            if (bhi >= r0 && bhi < r0 + 64) atomicOr(&s_last[bhi - r0], me);
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            unsigned long long f = s_first[lane], e = s_last[lane];
+            const unsigned long long f_in = __ballot(blo < r0);        // started before
+            const unsigned long long e_in = __ballot(bhi >= r0 + 64 && bhi != -1);  // ends after
 #pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const int v = __shfl_up(incl, off);
-            if (lane >= off) incl += v;
+            for (int off = 1; off < 64; off <<= 1) {
+                const unsigned long long fu = __shfl_up(f, off);
+                const unsigned long long ed = __shfl_down(e, off);
+                if (lane >= off) f |= fu;
+                if (lane + off < 64) e |= ed;
+            }
+            if (r0 + lane < n_bins)
+                out[(int64_t)(r0 + lane) * n_chunks + chunk] = (f | f_in) & (e | e_in);
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
         }
-        int pos = base + incl - cnt;
-        while (mine) {
-            live_ids[pos++] = (c0 + lane) * 64 + __builtin_ctzll(mine);
-            mine &= mine - 1ull;
-        }
-        base += __shfl(incl, 63);
-    }
-    if (lane == 0) {
-        *n_live = base;
-        __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    };
+    bin_words(b.y0 - row_begin, b.y1 - row_begin, n_cy, kCoarseH, row_masks);
+    bin_words(b.x0, b.x1, n_cx, kCoarseW, col_masks);
 }
 
 #if RT_TIMELINE
@@ -778,8 +784,9 @@ static_assert(kTiles <= 16 && kTmWords <= 4, "tile words");
 constexpr int kRound = RT_C3_ROUND;
 __global__ void __launch_bounds__(64) coarse3_kernel(
     const int4* __restrict__ boxes, const Cls* __restrict__ cls, int n_prims, int n_tri,
-    int n_cx, const int* __restrict__ live_ids, const int* __restrict__ n_live, int row_begin,
-    int half_cap, int* __restrict__ counts, int* __restrict__ lists) {
+    int n_cx, const unsigned long long* __restrict__ row_masks,
+    const unsigned long long* __restrict__ col_masks, int row_begin, int half_cap,
+    int* __restrict__ counts, int* __restrict__ lists) {
     __shared__ int s_ids[kRound];
     __shared__ unsigned s_tm[kRound * kTmWords];
     __shared__ int4 s_box[kRound];
@@ -863,37 +870,56 @@ __global__ void __launch_bounds__(64) coarse3_kernel(
         __builtin_amdgcn_wave_barrier();
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
     };
-    // scan all primitives, or (band renders) the compacted in-band list
-    const int n_scan = live_ids ? *n_live : n_prims;
-    for (int base = 0; base < n_scan; base += 64 * kBatch) {
-        int4 bb[kBatch];
-        int pid[kBatch];
-#pragma unroll
-        for (int k = 0; k < kBatch; ++k) {
-            const int e = base + 64 * k + lane;
-            pid[k] = e < n_scan ? (live_ids ? live_ids[e] : e) : -1;
+    // Stage the overlapping ids in primitive order (rounds of kRound).
+    auto stage = [&](unsigned long long m, int chunk_base) {
+        const int n_ov = __popcll(m);
+        if (n_ov == 0) return;
+        if (staged + n_ov > kRound) {
+            if (RT_C3_ABL == 0) classify_round(staged);  // diag: 1 = scan only
+            staged = 0;
         }
-#pragma unroll
-        for (int k = 0; k < kBatch; ++k)
-            bb[k] = pid[k] >= 0 ? boxes[RT_C3_ABL == 2 ? (pid[k] & 63) : pid[k]]
-                                : make_int4(1 << 30, 1 << 30, -(1 << 30), -(1 << 30));
-#pragma unroll
-        for (int k = 0; k < kBatch; ++k) {
-            const int4 b = bb[k];
-            const bool ov = b.x <= x1 && b.z >= x0 && b.y <= y1 && b.w >= y0;
-            const unsigned long long m = __ballot(ov);
-            const int n_ov = __popcll(m);
-            if (n_ov == 0) continue;
-            if (staged + n_ov > kRound) {
-                if (RT_C3_ABL == 0) classify_round(staged);  // diag: 1 = scan only
-                staged = 0;
+        if ((m >> lane) & 1ull) {
+            const unsigned below = __builtin_amdgcn_mbcnt_hi(
+                (unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+            s_ids[staged + (int)below] = chunk_base + lane;
+        }
+        staged += n_ov;
+    };
+    const int n_chunks = (n_prims + 63) / 64;
+    if (row_masks) {
+        // candidates = this bin row's chunk words AND this bin column's
+        const unsigned long long* rw = row_masks + (int64_t)(cb / n_cx) * n_chunks;
+        const unsigned long long* cw = col_masks + (int64_t)(cb % n_cx) * n_chunks;
+        // lane l loads chunk c0 + l's two words; the nonzero chunks are
+        // staged in order
+        for (int c0 = 0; c0 < n_chunks; c0 += 64) {
+            const int c = c0 + lane;
+            const unsigned long long w = c < n_chunks ? rw[c] & cw[c] : 0ull;
+            unsigned long long nz = __ballot(w != 0ull);
+            while (nz) {
+                const int l = __builtin_ctzll(nz);
+                nz &= nz - 1ull;
+                const unsigned long long m =
+                    (unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(unsigned)w, l) |
+                    ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(unsigned)(w >> 32), l) << 32);
+                stage(m, (c0 + l) * 64);
             }
-            if (ov) {
-                const unsigned below = __builtin_amdgcn_mbcnt_hi(
-                    (unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-                s_ids[staged + (int)below] = pid[k];
+        }
+    } else {
+        // scan every box (frames with too many bin rows + columns for masks)
+        for (int base = 0; base < n_prims; base += 64 * kBatch) {
+            int4 bb[kBatch];
+#pragma unroll
+            for (int k = 0; k < kBatch; ++k) {
+                const int e = base + 64 * k + lane;
+                bb[k] = e < n_prims ? boxes[RT_C3_ABL == 2 ? (e & 63) : e]
+                                    : make_int4(1 << 30, 1 << 30, -(1 << 30), -(1 << 30));
             }
-            staged += n_ov;
+#pragma unroll
+            for (int k = 0; k < kBatch; ++k) {
+                const int4 q = bb[k];
+                stage(__ballot(q.x <= x1 && q.z >= x0 && q.y <= y1 && q.w >= y0), base + 64 * k);
+            }
         }
     }
     if (staged && RT_C3_ABL == 0) classify_round(staged);
@@ -1182,6 +1208,7 @@ struct rt_ctx {
     // coarse lists take 4 B x kListStride x (primitives + 16) per 64x64 bin; a frame whose
     // lists would exceed this is rendered as internal row bands
     int64_t list_budget = (int64_t)4 << 30;
+    bool bin_masks = RT_BIN_MASKS != 0;  // separable bin masks (false: coarse scans every box)
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     // profiling: per render, start/stop events of the prep, coarse and trace
     // kernels, attached to the kernels' own dispatch packets
@@ -1259,7 +1286,7 @@ int skip_k(hipStream_t stream, const hipEvent_t* ev) {
 // Enqueue one render of rows [row_begin, row_end) on `stream`.  All scene
 // pointers are device pointers.
 int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origins,
-           int32_t width, int32_t row_begin, int32_t row_end, bool band, int32_t fmt,
+           int32_t width, int32_t row_begin, int32_t row_end, int32_t fmt,
            int32_t path, void* out, hipStream_t stream, int32_t* used_path) {
     SceneDev sd{reinterpret_cast<const float4*>(s->sphere_origins), s->sphere_radius,
                 reinterpret_cast<const float4*>(s->sphere_colours),
@@ -1273,7 +1300,7 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
     if (used_path) *used_path = use_bin ? RT_PATH_BINNED : RT_PATH_GENERIC;
     if (use_bin) {
         // Bound the candidate-list workspace: split into bands of whole
-        // coarse rows, each a band render (prep compacts to its primitives),
+        // coarse rows, each a band render (bin masks per band),
         // in order on the same stream.
         const int64_t n_prims = 12 * (int64_t)s->num_cubes + s->num_spheres;
         const int64_t row_bytes =
@@ -1286,8 +1313,8 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
             for (int64_t rb = row_begin; rb < row_end; rb += per) {
                 const int32_t re = (int32_t)std::min<int64_t>(rb + per, row_end);
                 char* dst = static_cast<char*>(out) + (size_t)(rb - row_begin) * width * px_bytes;
-                const int rc = launch(ctx, s, d, origins, width, (int32_t)rb, re, true, fmt, path,
-                                      dst, stream, nullptr);
+                const int rc = launch(ctx, s, d, origins, width, (int32_t)rb, re, fmt, path, dst,
+                                      stream, nullptr);
                 if (rc) return rc;
             }
             if (ctx->profile) ctx->prof_count = prof_count0 + 1;  // one render, summed bands
@@ -1338,9 +1365,10 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
     const size_t cnt_off =
         col_off + align_up(sizeof(float4) * (size_t)(s->num_cubes + s->num_spheres), 256);
     const int n_chunks = (n_prims + kPrepThreads - 1) / kPrepThreads;
-    const size_t live_off = cnt_off + align_up(sizeof(int) * (size_t)n_coarse, 256);
-    const size_t mask_off = live_off + align_up(sizeof(int) * ((size_t)n_prims + 64), 256);
-    const size_t rec_need = mask_off + align_up(sizeof(unsigned long long) * (size_t)n_chunks, 256);
+    const bool use_masks = ctx->bin_masks && (int64_t)n_cx + n_cy <= kMaskBinsMax;
+    const size_t mask_off = cnt_off + align_up(sizeof(int) * (size_t)n_coarse, 256);
+    const size_t n_mask_words = use_masks ? (size_t)n_chunks * (size_t)(n_cx + n_cy) : 0;
+    const size_t rec_need = mask_off + align_up(sizeof(unsigned long long) * n_mask_words, 256);
     rc = ensure(&ctx->rec_buf, &ctx->rec_cap, rec_need);
     if (rc) return rc;
     const size_t list_need = sizeof(int) * kListStride * (size_t)half_cap * (size_t)n_coarse + 256;
@@ -1353,11 +1381,9 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
     Cls* clsv = reinterpret_cast<Cls*>(base + cls_off);
     float4* colours = reinterpret_cast<float4*>(base + col_off);
     int* counts = reinterpret_cast<int*>(base + cnt_off);
-    // band compaction workspace: n_live, then the ordered in-band ids
-    int* n_live = reinterpret_cast<int*>(base + live_off);
-    int* live_ids = n_live + 64;
-    unsigned long long* chunk_masks = reinterpret_cast<unsigned long long*>(base + mask_off);
-    const bool compact = (band && RT_COMPACT != 0) || RT_COMPACT == 2;
+    unsigned long long* row_masks =
+        use_masks ? reinterpret_cast<unsigned long long*>(base + mask_off) : nullptr;
+    unsigned long long* col_masks = use_masks ? row_masks + (size_t)n_chunks * n_cy : nullptr;
     int* lists = static_cast<int*>(ctx->list_buf);
     // generation-stamped non-finite flag: no per-launch memset needed
     if (++ctx->gen == 0) {
@@ -1368,13 +1394,12 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
     if (n_prims > 0) {
         rc = launch_k(prep_kernel, dim3((unsigned)n_chunks), dim3(kPrepThreads), stream, pe_prep,
                       sd, dir, width, row_begin, row_end, tri, sph, boxes, clsv, colours,
-                      ctx->flag, ctx->gen, compact ? chunk_masks : nullptr, ctx->flag + 1,
-                      compact ? live_ids : nullptr, n_live);
+                      ctx->flag, ctx->gen, row_masks, col_masks, n_cx, n_cy);
         if (rc) return rc;
         rc = launch_k(coarse3_kernel, dim3((unsigned)n_coarse), dim3(64), stream, pe_coarse,
                       (const int4*)boxes, (const Cls*)clsv, n_prims, n_tri, n_cx,
-                      (const int*)(compact ? live_ids : nullptr), (const int*)n_live, row_begin,
-                      half_cap, counts, lists);
+                      (const unsigned long long*)row_masks, (const unsigned long long*)col_masks,
+                      row_begin, half_cap, counts, lists);
         if (rc) return rc;
     } else {
         if ((rc = skip_k(stream, pe_prep))) return rc;
@@ -1431,7 +1456,7 @@ int rt_init(int device_ordinal, rt_ctx** out_ctx) {
             return RT_ERR_HIP;
         }
     }
-    // [0] non-finite flag, [1] band-compaction arrival counter (zero between renders)
+    // [0] non-finite flag
     if (hipMalloc(&ctx->flag, 4 * sizeof(unsigned)) != hipSuccess ||
         hipMemset(ctx->flag, 0, 4 * sizeof(unsigned)) != hipSuccess) {
         rt_destroy(ctx);
@@ -1505,8 +1530,8 @@ int rt_render_path(rt_ctx* ctx, const rt_scene* scene, const float ray_dir[4],
     dscene.cube_colours = reinterpret_cast<const float*>(sb + o_cc);
     HIP_TRY(hipEventRecord(ctx->ev[1], st));
     int32_t used = 0;
-    rc = launch(ctx, &dscene, ray_dir, d_origins, width, row_begin, row_end,
-                row_begin > 0 || row_end < height, out_format, path, ctx->out_buf, st, &used);
+    rc = launch(ctx, &dscene, ray_dir, d_origins, width, row_begin, row_end, out_format, path,
+                ctx->out_buf, st, &used);
     if (rc) return rc;
     HIP_TRY(hipEventRecord(ctx->ev[2], st));
     HIP_TRY(hipMemcpyAsync(host_out, ctx->out_buf, out_bytes, hipMemcpyDeviceToHost, st));
@@ -1545,7 +1570,7 @@ int rt_render_device(rt_ctx* ctx, const rt_scene* device_scene, const float ray_
     HIP_TRY(hipSetDevice(ctx->device));
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
     return launch(ctx, device_scene, ray_dir, device_ray_origins, width, row_begin, row_end,
-                  row_begin > 0 || row_end < height, out_format, path, device_out, st, nullptr);
+                  out_format, path, device_out, st, nullptr);
 }
 
 int rt_profile_enable(rt_ctx* ctx, int enable) {
@@ -1628,6 +1653,12 @@ int rt_debug_triangle_box(const float v0[3], const float v1[3], const float v2[3
 int rt_debug_set_list_budget(rt_ctx* ctx, int64_t bytes) {
     if (!ctx || bytes < 0) return RT_ERR_INVALID_ARG;
     ctx->list_budget = bytes ? bytes : (int64_t)4 << 30;
+    return RT_OK;
+}
+
+int rt_debug_set_bin_masks(rt_ctx* ctx, int enable) {
+    if (!ctx) return RT_ERR_INVALID_ARG;
+    ctx->bin_masks = enable != 0;
     return RT_OK;
 }
 

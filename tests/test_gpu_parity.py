@@ -353,12 +353,11 @@ def test_headless_cpp_driver_bands(pkg, bands, tmp_path):
     assert np.array_equal(rgb, g["frame"][101:333, :, :3].astype(np.uint8))
 
 
-def test_band_compaction_weak_scaling_layout(pkg, rt, oracle):
+def test_band_renders_weak_scaling_layout(pkg, rt, oracle):
     """bench.py's N=8 weak-scaling layout at reduced size: a 1024 x 8192
-    frame with 8x the primitives, rendered as 8 row bands (band renders
-    compact the in-band primitives in prep; the arrival counter must reset
-    between renders) -- bit-identical to the full-frame render (no
-    compaction) and to the oracle on sampled rows."""
+    frame with 8x the primitives, rendered as 8 row bands (each band's bin
+    masks hold only its in-band primitives) -- bit-identical to the
+    full-frame render and to the oracle on sampled rows."""
     w, h, ranks = 1024, 8192, 8
     scene = pkg.Scene.synthetic(w, h, 64 * ranks, 16 * ranks, seed=8, k=w / 640)
     full, t = rt.render(scene, w, h)
@@ -370,6 +369,29 @@ def test_band_compaction_weak_scaling_layout(pkg, rt, oracle):
     for row in range(0, h, 509):
         want = oracle.trace(scene, w, h, rows=(row, row + 1), threads=THREADS)
         assert np.array_equal(full[row:row + 1], want), f"row {row}"
+
+
+@pytest.mark.parametrize("w,h,ns,nc,k", [(640, 480, 60, 12, 1.0), (1000, 777, 500, 40, 1.2),
+                                         (333, 4100, 200, 20, 2.0), (4160, 70, 300, 30, 3.0)])
+def test_bin_masks_match_box_scan(pkg, rt, oracle, w, h, ns, nc, k):
+    """Coarse binning from the separable bin-row / bin-column masks equals
+    the scan of every box (the extreme-aspect path), on full frames and row
+    bands, and both match the oracle."""
+    scene = pkg.Scene.synthetic(w, h, ns, nc, seed=w + h, k=k)
+    try:
+        frames = {}
+        for masks in (True, False):
+            rt.set_bin_masks(masks)
+            full, t = rt.render(scene, w, h)
+            assert t.path == "binned"
+            band, _ = rt.render(scene, w, h, rows=(h // 3, h - h // 5))
+            assert np.array_equal(band, full[h // 3:h - h // 5])
+            frames[masks] = full
+    finally:
+        rt.set_bin_masks(True)
+    assert np.array_equal(frames[True], frames[False])
+    want = oracle.trace(scene, w, h, threads=THREADS)
+    assert not diff_report(frames[True], want), diff_report(frames[True], want)
 
 
 def test_error_paths_on_device(pkg, rt):
@@ -476,8 +498,8 @@ def test_maximum_size_frames(pkg, rt, oracle):
 
 def test_list_budget_bands(pkg, rt, oracle):
     """Frames whose coarse candidate lists would pass the workspace budget
-    render as internal bands of whole coarse rows (band renders, compacted
-    prep), one after another on the stream: bit-identical to the unsplit
+    render as internal bands of whole coarse rows (band renders with their
+    own bin masks), one after another on the stream: bit-identical to the unsplit
     frame, for full frames, row ranges and both formats."""
     w, h = 1000, 777
     scene = pkg.Scene.synthetic(w, h, 500, 40, seed=31, k=1.2)
