@@ -49,8 +49,9 @@ def parse():
     ap.add_argument("--seed", type=int, default=3)
     ap.add_argument("--k", type=float, default=None, help="object scale (default width/640)")
     ap.add_argument("--format", choices=sorted(BYTES_PER_RAY), default="i32x4")
-    ap.add_argument("--cpu-rows", type=int, default=4,
-                    help="CPU baseline samples every Nth row of rank 0's band")
+    ap.add_argument("--cpu-rows", type=int, default=1,
+                    help="CPU baseline samples every Nth row of rank 0's band (1 = the "
+                         "whole band: the full config-3 frame at N=1, ~4 s on 16 threads)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
@@ -229,9 +230,10 @@ def main():
         c_s = time.perf_counter() - c0
         cpu = {"value": len(sample_rows) * w / c_s / 1e6, "unit": "Mrays/s", "cores": threads,
                "kind": "port",
-               "sample": f"{len(sample_rows)} rows (every {args.cpu_rows}th of rank 0's band) x {w}"
-                         f" px of the same scene, oracle/rt_oracle.c orc_trace_rows_mt on "
-                         f"{threads} threads, {c_s:.1f} s"}
+               "sample": (f"the whole {w}x{len(sample_rows)} frame" if args.cpu_rows == 1 else
+                          f"{len(sample_rows)} rows (every {args.cpu_rows}th of rank 0's band) x {w}"
+                          f" px") + f" of the same scene, oracle/rt_oracle.c orc_trace_rows_mt on "
+                         f"{threads} threads, {c_s:.1f} s wall"}
 
     if rank == 0:
         line = {
