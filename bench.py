@@ -132,34 +132,46 @@ def main():
     barrier()
     torch.cuda.synchronize(dev)
 
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps):
-        step()
-    ev1.record(stream)
-    torch.cuda.synchronize(dev)
-    barrier()
-    torch.cuda.synchronize(dev)
-    wall_ms = (time.perf_counter() - t0) * 1e3 / args.steps
-    event_ms = ev0.elapsed_time(ev1) / args.steps
-    if distributed:
-        tt = torch.tensor([wall_ms], device=coll_dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        wall_ms = float(tt.item())
+    def timed(profiled: bool):
+        """K steps between barrier + sync on both sides; wall ms per step
+        (max over ranks) and the stream-event ms per step."""
+        rt.profile(profiled)
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize(dev)
+        barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        for _ in range(args.steps):
+            step()
+        ev1.record(stream)
+        torch.cuda.synchronize(dev)
+        barrier()
+        torch.cuda.synchronize(dev)
+        wall = (time.perf_counter() - t0) * 1e3 / args.steps
+        rt.profile(False)
+        if distributed:
+            tt = torch.tensor([wall], device=coll_dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            wall = float(tt.item())
+        return wall, ev0.elapsed_time(ev1) / args.steps
 
-    # Per-kernel durations: a second, profiled pass.  librt_hip.so attaches
-    # start/stop HIP events to each kernel's own dispatch packet on the launch
-    # stream (hipExtLaunchKernelGGL), so they time the kernel itself.
+    # The timed region.  librt_hip.so attaches start/stop HIP events to each
+    # kernel's own dispatch packet on the launch stream (hipExtLaunchKernelGGL,
+    # events from a pool created in warmup), so the per-kernel durations come
+    # from these same K steps without extra queue packets between kernels.
     rt.profile(True)
-    for _ in range(args.steps):
+    for _ in range(args.steps):  # untimed: grows the event pool to K renders
         step()
     torch.cuda.synchronize(dev)
+    rt.profile_read()
+    wall_ms, event_ms = timed(True)
     prof = rt.profile_read()
-    rt.profile(False)
     n = max(prof["renders"], 1)
     trace_ms = prof["trace_ms"] / n
     prep_ms, bin_ms = prof["prep_ms"] / n, prof["bin_ms"] / n
+    # the same K steps without the attached events, reported beside
+    plain_ms, _ = timed(False)
 
     rays_rank = w * rows
     value = world * rays_rank / (wall_ms * 1e-3) / 1e6
@@ -254,6 +266,7 @@ def main():
                          "kernel_ms": round(trace_ms, 4), "prep_ms": round(prep_ms, 4),
                          "bin_ms": round(bin_ms, 4), "algo_bytes_per_launch": algo_bytes},
             "event_ms_per_step": round(event_ms, 4),
+            "unprofiled_ms_per_step": round(plain_ms, 4),
             "cpu_baseline": cpu,
             "gather": gather,
             "host_path": host,

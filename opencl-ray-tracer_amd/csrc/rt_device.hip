@@ -1213,7 +1213,8 @@ struct rt_ctx {
     // profiling: per render, start/stop events of the prep, coarse and trace
     // kernels, attached to the kernels' own dispatch packets
     bool profile = false;
-    std::vector<hipEvent_t> prof_events;
+    std::vector<hipEvent_t> prof_events;  // a pool: created once, reused
+    size_t prof_used = 0;                 // events holding this batch's timestamps
     int32_t prof_count = 0;
 };
 
@@ -1323,12 +1324,13 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
     }
     const hipEvent_t* pe = nullptr;  // 6 events: prep, coarse, trace (start, stop)
     if (ctx->profile) {
-        for (int k = 0; k < 6; ++k) {
+        while (ctx->prof_events.size() < ctx->prof_used + 6) {
             hipEvent_t e;
             HIP_TRY(hipEventCreate(&e));
             ctx->prof_events.push_back(e);
         }
-        pe = &ctx->prof_events[ctx->prof_events.size() - 6];
+        pe = &ctx->prof_events[ctx->prof_used];
+        ctx->prof_used += 6;
         ++ctx->prof_count;
     }
     const hipEvent_t* pe_prep = pe ? pe : nullptr;
@@ -1584,7 +1586,7 @@ int rt_profile_read(rt_ctx* ctx, double* prep_ms, double* bin_ms, double* trace_
     if (!ctx) return RT_ERR_INVALID_ARG;
     HIP_TRY(hipSetDevice(ctx->device));
     double sums[3] = {0, 0, 0};
-    for (size_t q = 0; q + 5 < ctx->prof_events.size(); q += 6) {
+    for (size_t q = 0; q + 5 < ctx->prof_used; q += 6) {
         HIP_TRY(hipEventSynchronize(ctx->prof_events[q + 5]));
         for (int k = 0; k < 3; ++k) {
             float ms = 0.0f;
@@ -1597,8 +1599,7 @@ int rt_profile_read(rt_ctx* ctx, double* prep_ms, double* bin_ms, double* trace_
     if (bin_ms) *bin_ms = sums[1];
     if (trace_ms) *trace_ms = sums[2];
     if (n_renders) *n_renders = ctx->prof_count;
-    for (auto e : ctx->prof_events) (void)hipEventDestroy(e);
-    ctx->prof_events.clear();
+    ctx->prof_used = 0;  // the events stay in the pool
     ctx->prof_count = 0;
     return RT_OK;
 }
