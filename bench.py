@@ -156,22 +156,25 @@ def main():
             wall = float(tt.item())
         return wall, ev0.elapsed_time(ev1) / args.steps
 
-    # The timed region.  librt_hip.so attaches start/stop HIP events to each
-    # kernel's own dispatch packet on the launch stream (hipExtLaunchKernelGGL,
-    # events from a pool created in warmup), so the per-kernel durations come
-    # from these same K steps without extra queue packets between kernels.
+    # The timed region: K steps, nothing attached to the kernels.
+    wall_ms, event_ms = timed(False)
+
+    # Per-kernel durations: the same K steps again with start/stop HIP events
+    # attached to each kernel's own dispatch packet on the launch stream
+    # (hipExtLaunchKernelGGL; events from a pool grown in an untimed pass).
+    # Not the timed region itself: with the events attached the wall time per
+    # step grows by 25-40% (58-60 -> 73-85 us measured), while the kernels'
+    # own durations agree with rocprofv3's.
     rt.profile(True)
     for _ in range(args.steps):  # untimed: grows the event pool to K renders
         step()
     torch.cuda.synchronize(dev)
     rt.profile_read()
-    wall_ms, event_ms = timed(True)
+    prof_wall_ms, _ = timed(True)
     prof = rt.profile_read()
     n = max(prof["renders"], 1)
     trace_ms = prof["trace_ms"] / n
     prep_ms, bin_ms = prof["prep_ms"] / n, prof["bin_ms"] / n
-    # the same K steps without the attached events, reported beside
-    plain_ms, _ = timed(False)
 
     rays_rank = w * rows
     value = world * rays_rank / (wall_ms * 1e-3) / 1e6
@@ -266,7 +269,7 @@ def main():
                          "kernel_ms": round(trace_ms, 4), "prep_ms": round(prep_ms, 4),
                          "bin_ms": round(bin_ms, 4), "algo_bytes_per_launch": algo_bytes},
             "event_ms_per_step": round(event_ms, 4),
-            "unprofiled_ms_per_step": round(plain_ms, 4),
+            "profiled_pass_ms_per_step": round(prof_wall_ms, 4),
             "cpu_baseline": cpu,
             "gather": gather,
             "host_path": host,

@@ -706,6 +706,7 @@ __device__ __forceinline__ void store_fmt(void* __restrict__ out, int64_t idx, i
 }
 
 // Shade (MainState.cpp:396-407) one lane's kRowsPerLane pixels.
+template <int kMode = 0>
 __device__ __forceinline__ void shade_pixels(const float4* __restrict__ colours,
                                              const float* closest, const int* hit, int4v* pix) {
     bool lane_hit = false;
@@ -717,7 +718,9 @@ __device__ __forceinline__ void shade_pixels(const float4* __restrict__ colours,
     if (any_hit) {
         float4 col[kRowsPerLane];
 #pragma unroll
-        for (int j = 0; j < kRowsPerLane; ++j) col[j] = colours[hit[j] >= 0 ? hit[j] : 0];
+        for (int j = 0; j < kRowsPerLane; ++j)  // kMode 4: no gather (diagnostics)
+            col[j] = kMode == 4 ? make_float4(1.0f, 0.5f, 0.25f, 255.0f)
+                                : colours[hit[j] >= 0 ? hit[j] : 0];
 #pragma unroll
         for (int j = 0; j < kRowsPerLane; ++j) {
             // lanes without a hit shade a dummy 1.0 (discarded) so that div180
@@ -1125,7 +1128,7 @@ __global__ void __launch_bounds__(64 * kTraceWaves) RT_TRACE_ATTR trace3_kernel(
 #if RT_TIMELINE
     tl2 = rt_now();
 #endif
-    shade_pixels(colours, closest, hit, pix);
+    shade_pixels<kMode>(colours, closest, hit, pix);
     } else {  // outside the frame: nothing is stored
 #pragma unroll
         for (int j = 0; j < kRowsPerLane; ++j) pix[j] = int4v{0, 0, 0, 255};
@@ -1412,10 +1415,12 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
                     ? (ctx->trace_mode == 1   ? trace3_kernel<1, RT_FORMAT_I32X4>
                        : ctx->trace_mode == 2 ? trace3_kernel<2, RT_FORMAT_I32X4>
                        : ctx->trace_mode == 3 ? trace3_kernel<3, RT_FORMAT_I32X4>
+                       : ctx->trace_mode == 4 ? trace3_kernel<4, RT_FORMAT_I32X4>
                                               : trace3_kernel<0, RT_FORMAT_I32X4>)
                     : (ctx->trace_mode == 1   ? trace3_kernel<1, RT_FORMAT_RGBA8>
                        : ctx->trace_mode == 2 ? trace3_kernel<2, RT_FORMAT_RGBA8>
                        : ctx->trace_mode == 3 ? trace3_kernel<3, RT_FORMAT_RGBA8>
+                       : ctx->trace_mode == 4 ? trace3_kernel<4, RT_FORMAT_RGBA8>
                                               : trace3_kernel<0, RT_FORMAT_RGBA8>);
     return launch_k(kern, dim3((unsigned)n_wgs), dim3(64 * kTraceWaves), stream, pe_trace, sd,
                     (const TriRec*)tri, (const SphRec*)sph, (const float4*)colours,
@@ -1664,7 +1669,7 @@ int rt_debug_set_bin_masks(rt_ctx* ctx, int enable) {
 }
 
 int rt_debug_set_trace_mode(rt_ctx* ctx, int mode) {
-    if (!ctx || mode < 0 || mode > 3) return RT_ERR_INVALID_ARG;
+    if (!ctx || mode < 0 || mode > 4) return RT_ERR_INVALID_ARG;
     ctx->trace_mode = mode;
     return RT_OK;
 }
