@@ -1,0 +1,31 @@
+/* Why the cube build stays on the host:
+ * Cube::rotate (Cube.cpp:53-64) takes glm::rotate's cos/sin of float angles,
+ * i.e. glibc cosf/sinf.  A device build would need those bit for bit, but
+ * glibc's sinf/cosf are not correctly rounded: this counts the floats in
+ * [-8, 8] where they differ from the correctly rounded (float)sin((double)x)
+ * (which a device libm could match).
+ *   gcc -O2 -ffp-contract=off -o check_glibc_sincos check_glibc_sincos.c -lm */
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+int main(void) {
+    uint64_t n = 0, bad_sin = 0, bad_cos = 0;
+    for (int sign = 0; sign < 2; ++sign) {
+        for (uint32_t b = 0; b < 0x7f800000u; ++b) {
+            const uint32_t u = b | (sign ? 0x80000000u : 0u);
+            float x;
+            memcpy(&x, &u, 4);
+            if (fabsf(x) > 8.0f) break;
+            const float s = sinf(x), c = cosf(x);
+            const float s2 = (float)sin((double)x), c2 = (float)cos((double)x);
+            bad_sin += memcmp(&s, &s2, 4) != 0;
+            bad_cos += memcmp(&c, &c2, 4) != 0;
+            ++n;
+        }
+    }
+    printf("floats in [-8, 8]: %llu; sinf != RN(sin): %llu; cosf != RN(cos): %llu\n",
+           (unsigned long long)n, (unsigned long long)bad_sin, (unsigned long long)bad_cos);
+    return 0;
+}
