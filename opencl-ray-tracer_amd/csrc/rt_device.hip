@@ -13,9 +13,9 @@
 //          which the exact test provably rejects.
 //   coarse one wave per 64x64 coarse bin: the ordered list of primitives
 //          whose box touches the bin (ballot + mbcnt, the reference's
-//          primitive order), each with a word of 2 bits per 8x32 wave tile
+//          primitive order), each with a word of 2 bits per 16x16 wave tile
 //          of the bin (tile classifier: skip / test / u,v proven inside).
-//   trace  one wave per 8x32 tile, four pixels per lane (rows 8 apart):
+//   trace  one wave per 16x16 tile, four pixels per lane (rows 4 apart):
 //          count, ids, tile words and records all on scalar loads, exact
 //          per-lane tests, 16-B coalesced framebuffer stores.
 // Plus `generic`, a brute-force per-pixel kernel for arbitrary ray origins
@@ -43,7 +43,8 @@ namespace {
 
 // Build-time geometry / feature knobs (A/B variants: scripts/variants.sh).
 #ifndef RT_TILE_W
-#define RT_TILE_W 8               // wave tile width (lanes per row)
+#define RT_TILE_W 16              // wave tile width (lanes per row); 8 (8x32 tiles) measured
+                                  // 1.9 us per frame slower at config 3
 #endif
 #ifndef RT_ROWS
 #define RT_ROWS 4                 // pixels per lane (rows, 64/RT_TILE_W apart)
