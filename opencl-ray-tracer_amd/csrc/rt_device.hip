@@ -767,6 +767,8 @@ constexpr int kListStride = 1 + kTmWords;
 static_assert(kTiles <= 16 && kTmWords <= 4, "tile words");
 
 // Coarse binning with per-block classification: one wave per coarse bin.
+// counts[cb] = -1 flags a frame whose scene data is not finite (prep's
+// generation-stamped flag): the trace then runs the reference verbatim.
 // (1) the ids whose box touches the coarse bin are compacted, in primitive
 // order, into LDS (rounds of kRound); (2) the (candidate, tile) pairs are
 // spread over the lanes, 16 lanes per candidate, each testing box overlap +
@@ -790,8 +792,12 @@ __global__ void __launch_bounds__(64) coarse3_kernel(
     const int4* __restrict__ boxes, const Cls* __restrict__ cls, int n_prims, int n_tri,
     int n_cx, const unsigned long long* __restrict__ row_masks,
     const unsigned long long* __restrict__ col_masks, int row_begin, int half_cap,
-    int* __restrict__ counts, int* __restrict__ lists) {
+    const unsigned* __restrict__ nonfinite_flag, unsigned gen, int* __restrict__ counts,
+    int* __restrict__ lists) {
     __shared__ int s_ids[kRound];
+    // read early (independent of the scan): a non-finite scene is handed to
+    // the trace as count -1, so the trace's first scalar load tells it both
+    const bool nonfinite = *nonfinite_flag == gen;
     __shared__ unsigned s_tm[kRound * kTmWords];
     __shared__ int4 s_box[kRound];
     __shared__ Cls s_cls[kRound];
@@ -928,7 +934,7 @@ __global__ void __launch_bounds__(64) coarse3_kernel(
     }
     if (staged && RT_C3_ABL == 0) classify_round(staged);
     if (RT_C3_ABL != 0 && lane == 0) out_tm[0] = staged;  // keep the scan; lists stay empty
-    if (lane == 0) counts[cb] = count;
+    if (lane == 0) counts[cb] = nonfinite ? -1 : count;
 }
 
 #if RT_TRACE_WAVES > 0
@@ -988,8 +994,7 @@ template <int kMode, int kFmt>
 __global__ void __launch_bounds__(64 * kTraceWaves) RT_TRACE_ATTR trace3_kernel(
     SceneDev scene, const TriRec* __restrict__ tri, const SphRec* __restrict__ sph,
     const float4* __restrict__ colours, const int* __restrict__ counts,
-    const int* __restrict__ lists, int half_cap, const unsigned* __restrict__ nonfinite_flag,
-    unsigned gen, float4 dir, int width, int row_begin, int row_end, int n_tiles_x, int n_cx,
+    const int* __restrict__ lists, int half_cap, float4 dir, int width, int row_begin, int row_end, int n_tiles_x, int n_cx,
     int out_format, void* __restrict__ out) {
     // workgroup = kTraceWaves tiles of one coarse bin (independent waves on
     // one CU: the candidate records one wave loads are scalar-cache hits for
@@ -1044,7 +1049,10 @@ __global__ void __launch_bounds__(64 * kTraceWaves) RT_TRACE_ATTR trace3_kernel(
     const int w_self = (int)(threadIdx.x >> 6);
 #endif
 
-    if (tile_in && kMode == 0 && *nonfinite_flag == gen) {
+    // the bin's count (-1: non-finite scene data, see coarse3_kernel) is the
+    // wave's first data load
+    const int count_raw = kMode == 1 ? 0 : counts[cb];
+    if (tile_in && kMode == 0 && count_raw < 0) {
         // Non-finite scene data: run the reference algorithm verbatim.
 #pragma unroll 1
         for (int j = 0; j < kRowsPerLane; ++j) {
@@ -1080,7 +1088,7 @@ __global__ void __launch_bounds__(64 * kTraceWaves) RT_TRACE_ATTR trace3_kernel(
     unsigned tile_max_key = order_key(kFar);
     bool dirty = false;
 #endif
-    const int count = kMode == 1 ? 0 : counts[cb];
+    const int count = count_raw < 0 ? 0 : count_raw;
     const int* __restrict__ ids = lists + (int64_t)cb * kListStride * half_cap;
     const int* __restrict__ tms = ids + (1 + t / kTilesPerWord) * half_cap;  // this tile's word
     const int tm_shift = kTileBits * (t % kTilesPerWord);
@@ -1405,7 +1413,7 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
         rc = launch_k(coarse3_kernel, dim3((unsigned)n_coarse), dim3(64), stream, pe_coarse,
                       (const int4*)boxes, (const Cls*)clsv, n_prims, n_tri, n_cx,
                       (const unsigned long long*)row_masks, (const unsigned long long*)col_masks,
-                      row_begin, half_cap, counts, lists);
+                      row_begin, half_cap, (const unsigned*)ctx->flag, ctx->gen, counts, lists);
         if (rc) return rc;
     } else {
         if ((rc = skip_k(stream, pe_prep))) return rc;
@@ -1425,8 +1433,7 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
                                               : trace3_kernel<0, RT_FORMAT_RGBA8>);
     return launch_k(kern, dim3((unsigned)n_wgs), dim3(64 * kTraceWaves), stream, pe_trace, sd,
                     (const TriRec*)tri, (const SphRec*)sph, (const float4*)colours,
-                    (const int*)counts, (const int*)lists, half_cap, (const unsigned*)ctx->flag,
-                    ctx->gen, dir, width, row_begin, row_end, n_tiles_x, n_cx, fmt, out);
+                    (const int*)counts, (const int*)lists, half_cap, dir, width, row_begin, row_end, n_tiles_x, n_cx, fmt, out);
 }
 
 }  // namespace
