@@ -946,6 +946,9 @@ __global__ void __launch_bounds__(64) coarse3_kernel(
 #ifndef RT_XCD_REMAP
 #define RT_XCD_REMAP 0  // trace: contiguous tile runs per XCD (T1 swizzle)
 #endif
+#ifndef RT_SPEC_BATCH
+#define RT_SPEC_BATCH 0  // trace: first list batch loaded beside the count
+#endif
 #ifndef RT_DEPTH_CULL
 #define RT_DEPTH_CULL 1  // skip spheres that cannot beat any lane's closest
 #endif
@@ -1052,6 +1055,21 @@ __global__ void __launch_bounds__(64 * kTraceWaves) RT_TRACE_ATTR trace3_kernel(
     // the bin's count (-1: non-finite scene data, see coarse3_kernel) is the
     // wave's first data load
     const int count_raw = kMode == 1 ? 0 : counts[cb];
+#if RT_SPEC_BATCH
+    // the list's first batch of ids / tile words, loaded beside the count
+    // (in bounds whatever the count: half_cap >= 8)
+    const int* __restrict__ ids = lists + (int64_t)cb * kListStride * half_cap;
+    const int* __restrict__ tms = ids + (1 + t / kTilesPerWord) * half_cap;  // this tile's word
+    int idv[8], tmv[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        idv[k] = ids[k];
+        tmv[k] = tms[k];
+    }
+#ifndef RT_SPEC_NOASM
+    asm volatile("" ::"s"(count_raw), "s"(idv[0]), "s"(tmv[0]));
+#endif
+#endif
     if (tile_in && kMode == 0 && count_raw < 0) {
         // Non-finite scene data: run the reference algorithm verbatim.
 #pragma unroll 1
@@ -1089,18 +1107,26 @@ __global__ void __launch_bounds__(64 * kTraceWaves) RT_TRACE_ATTR trace3_kernel(
     bool dirty = false;
 #endif
     const int count = count_raw < 0 ? 0 : count_raw;
+#if !RT_SPEC_BATCH
     const int* __restrict__ ids = lists + (int64_t)cb * kListStride * half_cap;
     const int* __restrict__ tms = ids + (1 + t / kTilesPerWord) * half_cap;  // this tile's word
+#endif
     const int tm_shift = kTileBits * (t % kTilesPerWord);
 #if RT_TIMELINE
     tl1 = rt_now();
 #endif
     for (int i0 = 0; i0 < count; i0 += 8) {
+#if RT_SPEC_BATCH
+        if (i0 > 0) {
+#else
         int idv[8], tmv[8];
+        {
+#endif
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            idv[k] = ids[i0 + k];  // half_cap is a multiple of 8 past the count
-            tmv[k] = tms[i0 + k];
+            for (int k = 0; k < 8; ++k) {
+                idv[k] = ids[i0 + k];  // half_cap is a multiple of 8 past the count
+                tmv[k] = tms[i0 + k];
+            }
         }
         const int n = min(8, count - i0);
 #pragma unroll
