@@ -146,9 +146,12 @@ def main():
             step()
         ev1.record(stream)
         torch.cuda.synchronize(dev)
+        # this rank's K steps end here; the trailing barrier's own latency
+        # (an RCCL all-reduce, tens of us) is not part of them.  The max over
+        # ranks below is the job's time: every rank started at the barrier.
+        wall = (time.perf_counter() - t0) * 1e3 / args.steps
         barrier()
         torch.cuda.synchronize(dev)
-        wall = (time.perf_counter() - t0) * 1e3 / args.steps
         rt.profile(False)
         if distributed:
             tt = torch.tensor([wall], device=coll_dev)
