@@ -165,6 +165,40 @@ int rt_scene_synthetic(int32_t width, int32_t height, int32_t num_spheres,
                        float* sphere_colours, float* cube_vertices,
                        float* cube_colours);
 
+/* ---- scene build on the device ---------------- */
+
+/* One Cube method call (Cube.cpp:53-83): scale(vec3), rotate(vec3) with
+ * angles in RADIANS (Rz * Ry * Rx, as Cube::rotate), translate(vec3). */
+enum { RT_CUBE_SCALE = 1, RT_CUBE_ROTATE = 2, RT_CUBE_TRANSLATE = 3 };
+typedef struct rt_cube_op {
+    int32_t op;
+    float x, y, z;
+} rt_cube_op;
+
+/* Replaces building `cubes` on the host (Cube::Cube + its transform calls,
+ * MainState.cpp:434-593, :617-638) followed by the vertex upload of
+ * executeRayTracerOpenCL (MainState.cpp:646-658, :796-816).  Cube c starts
+ * from device_vertices_in[36c .. 36c+35] (float4), or from Cube::Cube's unit
+ * cube when device_vertices_in is NULL, and applies
+ * device_ops[device_op_offsets[c] .. device_op_offsets[c+1]) in order; the
+ * result goes to device_vertices_out (float4[36 * num_cubes], may equal
+ * device_vertices_in).  Bit-identical to the rt_cube_* host functions (glibc
+ * cosf/sinf restated on the device).  All pointers are device pointers;
+ * asynchronous on `stream` (NULL = the context's stream). */
+int rt_cube_build_device(rt_ctx* ctx, const rt_cube_op* device_ops,
+                         const int32_t* device_op_offsets, int32_t num_cubes,
+                         const float* device_vertices_in,
+                         float* device_vertices_out, void* stream);
+
+/* rt_scene_synthetic built on the device into device arrays: bit-identical
+ * arrays, no host build or upload.  Asynchronous on `stream`. */
+int rt_scene_synthetic_device(rt_ctx* ctx, int32_t width, int32_t height,
+                              int32_t num_spheres, int32_t num_cubes,
+                              uint64_t seed, float k, float* sphere_origins,
+                              float* sphere_radius, float* sphere_colours,
+                              float* cube_vertices, float* cube_colours,
+                              void* stream);
+
 /* Texture conversion (MainState.cpp:1023-1037) on the host. */
 void rt_pack_rgba8(const int32_t* frame, int64_t n_pixels, uint32_t* out);
 

@@ -59,6 +59,15 @@ int rt_debug_set_list_budget(rt_ctx* ctx, int64_t bytes);
  * more than 4096 bin rows + columns take). */
 int rt_debug_set_bin_masks(rt_ctx* ctx, int enable);
 
+/* Host evaluation of the device's restatement of glibc 2.35 sinf / cosf
+ * (the same __host__ __device__ code rt_cube_build_device runs), for the
+ * CPU test against the host's libm. */
+int rt_debug_glibc_sincosf(const float* x, int64_t n, float* sin_out,
+                           float* cos_out);
+/* The same restatement run on the device (synchronous; device pointers). */
+int rt_selftest_sincosf(rt_ctx* ctx, const float* device_in, int64_t n,
+                        float* device_sin, float* device_cos);
+
 #ifdef __cplusplus
 }
 #endif

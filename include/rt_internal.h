@@ -1,0 +1,17 @@
+/*
+ * rt_internal.h -- shared between the library's own translation units
+ * (rt_device.hip, rt_scene_device.hip).  Not installed, not part of the ABI.
+ */
+#ifndef RT_INTERNAL_H
+#define RT_INTERNAL_H
+
+#include <hip/hip_runtime.h>
+
+#include "rt_hip.h"
+
+namespace rt_internal {
+int ctx_device(const rt_ctx* ctx);
+hipStream_t ctx_stream(const rt_ctx* ctx);
+}  // namespace rt_internal
+
+#endif /* RT_INTERNAL_H */

@@ -24,7 +24,8 @@ __all__ = [
     "RT_ERR_UNSUPPORTED", "RT_FORMAT_I32X4", "RT_FORMAT_RGBA8", "RT_PATH_AUTO", "RT_PATH_BINNED",
     "RT_PATH_GENERIC", "RtError", "Scene", "Timing", "RayTracer", "MainState",
     "library", "library_path", "primary_ray_dir", "pack_rgba8", "cube_packed",
-    "deg_to_rad", "encode_png", "EXPORTED_SYMBOLS",
+    "deg_to_rad", "encode_png", "EXPORTED_SYMBOLS", "CUBE_OP_DTYPE", "cube_ops",
+    "debug_glibc_sincosf",
 ]
 
 PKG_DIR = Path(__file__).resolve().parent
@@ -42,7 +43,7 @@ EXPORTED_SYMBOLS = (
     "rt_render_device", "rt_profile_enable", "rt_profile_read", "rt_device_info",
     "rt_cube_init", "rt_cube_scale", "rt_cube_rotate", "rt_cube_translate",
     "rt_deg_to_rad", "rt_primary_ray_dir", "rt_scene_reference", "rt_scene_synthetic",
-    "rt_pack_rgba8", "rt_abi_version",
+    "rt_pack_rgba8", "rt_abi_version", "rt_cube_build_device", "rt_scene_synthetic_device",
 )
 
 
@@ -133,6 +134,11 @@ def library() -> ctypes.CDLL:
         "rt_debug_set_trace_mode": (ctypes.c_int, [vp, ctypes.c_int]),
         "rt_debug_set_list_budget": (ctypes.c_int, [vp, ctypes.c_int64]),
         "rt_debug_set_bin_masks": (ctypes.c_int, [vp, ctypes.c_int]),
+        "rt_cube_build_device": (ctypes.c_int, [vp, vp, vp, i32, vp, vp, vp]),
+        "rt_scene_synthetic_device": (ctypes.c_int, [vp, i32, i32, i32, i32, ctypes.c_uint64,
+                                                     f32, vp, vp, vp, vp, vp, vp]),
+        "rt_debug_glibc_sincosf": (ctypes.c_int, [vp, ctypes.c_int64, vp, vp]),
+        "rt_selftest_sincosf": (ctypes.c_int, [vp, vp, ctypes.c_int64, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -181,6 +187,30 @@ def cube_packed(ops) -> np.ndarray:
     for op, x, y, z in ops:
         fns[op](_ptr(v), x, y, z)
     return v
+
+
+# rt_cube_op (include/rt_hip.h): one Cube method call; rotate angles in radians
+CUBE_OP_DTYPE = np.dtype([("op", "<i4"), ("x", "<f4"), ("y", "<f4"), ("z", "<f4")])
+CUBE_OPS = {"scale": 1, "rotate": 2, "translate": 3}
+
+
+def cube_ops(programs) -> Tuple[np.ndarray, np.ndarray]:
+    """Pack per-cube op lists [[("scale"|"rotate"|"translate", x, y, z), ...], ...]
+    into the (rt_cube_op array, int32 offsets) pair rt_cube_build_device reads."""
+    flat = [(CUBE_OPS[op], x, y, z) for prog in programs for op, x, y, z in prog]
+    ops = np.array(flat, CUBE_OP_DTYPE) if flat else np.zeros(0, CUBE_OP_DTYPE)
+    offsets = np.zeros(len(programs) + 1, np.int32)
+    offsets[1:] = np.cumsum([len(p) for p in programs])
+    return ops, offsets
+
+
+def debug_glibc_sincosf(x: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+    """Host run of the device's restatement of glibc sinf / cosf."""
+    x = np.ascontiguousarray(x, np.float32).reshape(-1)
+    s, c = np.empty_like(x), np.empty_like(x)
+    _check(library().rt_debug_glibc_sincosf(_ptr(x), x.size, _ptr(s), _ptr(c)),
+           "rt_debug_glibc_sincosf")
+    return s, c
 
 
 def pack_rgba8(frame: np.ndarray) -> np.ndarray:
@@ -401,6 +431,31 @@ class RayTracer:
         _check(library().rt_device_info(self._ctx, name, 256, ctypes.byref(cu),
                                         ctypes.byref(mem)), "rt_device_info")
         return {"name": name.value.decode(), "cus": cu.value, "total_mem": mem.value}
+
+    def cube_build_device(self, ops_ptr: int, offsets_ptr: int, n_cubes: int,
+                          vertices_out_ptr: int, vertices_in_ptr: int = 0,
+                          stream: int = 0) -> None:
+        """rt_cube_build_device: cubes from the unit cube (or vertices_in) through
+        their rt_cube_op programs, on the device.  All device pointers."""
+        _check(library().rt_cube_build_device(self._ctx, ops_ptr or None, offsets_ptr or None,
+                                              n_cubes, vertices_in_ptr or None,
+                                              vertices_out_ptr or None, stream or None),
+               "rt_cube_build_device")
+
+    def scene_synthetic_device(self, width: int, height: int, n_spheres: int, n_cubes: int,
+                               seed: int, k: float, device_scene: dict, stream: int = 0) -> None:
+        """rt_scene_synthetic_device into the device arrays of `device_scene`
+        (rt_scene field name -> device address)."""
+        g = device_scene.get
+        _check(library().rt_scene_synthetic_device(
+            self._ctx, width, height, n_spheres, n_cubes, seed, k, g("sphere_origins"),
+            g("sphere_radius"), g("sphere_colours"), g("cube_vertices"), g("cube_colours"),
+            stream or None), "rt_scene_synthetic_device")
+
+    def selftest_sincosf(self, x_ptr: int, n: int, sin_ptr: int, cos_ptr: int) -> None:
+        """The device's glibc sinf / cosf restatement on n device floats."""
+        _check(library().rt_selftest_sincosf(self._ctx, x_ptr, n, sin_ptr, cos_ptr),
+               "rt_selftest_sincosf")
 
     def selftest_fp32(self, x: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
         x = np.ascontiguousarray(x, np.float32)

@@ -36,6 +36,7 @@
 
 #include "rt_hip.h"
 #include "rt_hip_debug.h"
+#include "rt_internal.h"
 
 #pragma clang fp contract(off)
 
@@ -1255,6 +1256,11 @@ struct rt_ctx {
     size_t prof_used = 0;                 // events holding this batch's timestamps
     int32_t prof_count = 0;
 };
+
+namespace rt_internal {
+int ctx_device(const rt_ctx* ctx) { return ctx->device; }
+hipStream_t ctx_stream(const rt_ctx* ctx) { return ctx->stream; }
+}  // namespace rt_internal
 
 namespace {
 

@@ -743,3 +743,12 @@ void orc_trace_cl32(int32_t width, int32_t height, const float ray_dir[4], int32
         }
     }
 }
+
+/* glm::rotate's cos / sin of a float angle (matrix_transform.inl:52-58):
+ * std::cos(float) -> the host libm's cosf / sinf. */
+void orc_libm_sincosf(const float* x, int64_t n, float* s, float* c) {
+    for (int64_t i = 0; i < n; ++i) {
+        s[i] = sinf(x[i]);
+        c[i] = cosf(x[i]);
+    }
+}

@@ -117,6 +117,10 @@ void orc_sphere_grid(const float centre[4], float radius, const float dir[4],
                      int32_t x0, int32_t y0, int32_t w, int32_t h, uint8_t* hits);
 
 /* FNV-1a-64 over the int32 stream (SURVEY.md §8c known-answer format). */
+/* The host libm's sinf / cosf on n floats: what glm::rotate's std::cos /
+ * std::sin (matrix_transform.inl:52-58) compute in the reference's CPU
+ * build; the checker of the device's glibc restatement. */
+void orc_libm_sincosf(const float* x, int64_t n, float* s, float* c);
 uint64_t orc_fnv1a_i32(const int32_t* v, int64_t n);
 
 /* Texture packing, MainState.cpp:1023-1037 + masks :984-994:

@@ -1,9 +1,10 @@
-/* Why the cube build stays on the host:
- * Cube::rotate (Cube.cpp:53-64) takes glm::rotate's cos/sin of float angles,
- * i.e. glibc cosf/sinf.  A device build would need those bit for bit, but
- * glibc's sinf/cosf are not correctly rounded: this counts the floats in
- * [-8, 8] where they differ from the correctly rounded (float)sin((double)x)
- * (which a device libm could match).
+/* Why the device scene build restates glibc instead
+ * of using a device libm: Cube::rotate (Cube.cpp:53-64) takes glm::rotate's
+ * cos/sin of float angles, i.e. glibc cosf/sinf, and those are not
+ * correctly rounded.  This counts the floats in [-8, 8] where they differ
+ * from the correctly rounded (float)sin((double)x), which is all a correctly
+ * rounded device libm could give.  The restatement that does match is
+ * checked by scripts/check_glibc_sincosf.c.
  *   gcc -O2 -ffp-contract=off -o check_glibc_sincos check_glibc_sincos.c -lm */
 #include <math.h>
 #include <stdint.h>

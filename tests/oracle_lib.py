@@ -56,6 +56,7 @@ def _load() -> ctypes.CDLL:
         "orc_tri_grid": (None, [_vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp]),
         "orc_sphere_grid": (None, [_vp, _f32, _vp, _i32, _i32, _i32, _i32, _vp]),
         "orc_fnv1a_i32": (ctypes.c_uint64, [_vp, ctypes.c_int64]),
+        "orc_libm_sincosf": (None, [_vp, ctypes.c_int64, _vp, _vp]),
         "orc_pack_rgba8": (None, [_vp, ctypes.c_int64, _vp]),
         "orc_srand": (None, [ctypes.c_uint]),
         "orc_get_float": (_f32, [_f32, _f32]),
@@ -195,6 +196,13 @@ class Oracle:
         for op, x, y, z in ops:
             fn[op](_p(v), x, y, z)
         return v
+
+    def libm_sincosf(self, x: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+        """The host libm's sinf / cosf (what glm::rotate computes)."""
+        x = np.ascontiguousarray(x, np.float32).reshape(-1)
+        s, c = np.empty_like(x), np.empty_like(x)
+        self.lib.orc_libm_sincosf(_p(x), x.size, _p(s), _p(c))
+        return s, c
 
     def deg2rad(self, d: float) -> float:
         return float(self.lib.orc_deg2rad(d))
