@@ -34,7 +34,7 @@ def main(path, mode=0, width=4096, height=4096, spheres=256, cubes=64, seed=3):
         [ctypes.c_int32] * 6 + [ctypes.c_void_p, ctypes.c_void_p]
     d = pkg.primary_ray_dir()
     out = torch.empty((height, width, 4), dtype=torch.int32, device=dev)
-    n_waves = (width // 8) * (height // 32)
+    n_waves = width * height // 256  # 256-pixel wave tiles
     tl = torch.zeros((n_waves * 8,), dtype=torch.int32, device=dev)
     assert lib.rt_debug_set_timeline(ctx, ctypes.c_void_p(tl.data_ptr())) == 0
     assert lib.rt_debug_set_trace_mode(ctx, mode) == 0
@@ -66,13 +66,20 @@ def main(path, mode=0, width=4096, height=4096, spheres=256, cubes=64, seed=3):
     pct(t3 - t2, "shade+store issue")
     # occupancy: waves alive per SIMD over time
     edges = np.linspace(0, span, 21)
-    print("time(us)  alive-waves/SIMD  started  finished")
+    print("time(us)  alive-waves/SIMD  started  finished  store-issue TB/s  mean walk of finished")
+    tile_bytes = width * height * 16 // n_waves
     for a, b in zip(edges[:-1], edges[1:]):
         mid = (a + b) / 2
         alive = ((t0 <= mid) & (t3 > mid)).sum() / 1024
         started = ((t0 >= a) & (t0 < b)).sum()
-        ended = ((t3 >= a) & (t3 < b)).sum()
-        print(f"{mid * us:7.1f}  {alive:8.2f}  {started:8d}  {ended:8d}")
+        fin = (t3 >= a) & (t3 < b)
+        ended = fin.sum()
+        rate = ended * tile_bytes / ((b - a) * us * 1e-6) / 1e12
+        walk = (t2 - t1)[fin].mean() * us if ended else 0.0
+        print(f"{mid * us:7.1f}  {alive:8.2f}  {started:8d}  {ended:8d}  {rate:8.2f}  {walk:8.2f}")
+    first = np.sort(t3)[:64]
+    print(f"first store issue at {first[0] * us:.2f} us, 64th at {first[-1] * us:.2f} us; "
+          f"first wave entry at {t0.min() * us:.2f} us")
     # dispatch order
     order = np.argsort(t0, kind="stable")
     wg = np.arange(n_waves) // 4
