@@ -134,6 +134,7 @@ def library() -> ctypes.CDLL:
         "rt_debug_set_trace_mode": (ctypes.c_int, [vp, ctypes.c_int]),
         "rt_debug_set_list_budget": (ctypes.c_int, [vp, ctypes.c_int64]),
         "rt_debug_set_bin_masks": (ctypes.c_int, [vp, ctypes.c_int]),
+        "rt_debug_set_small_path": (ctypes.c_int, [vp, ctypes.c_int]),
         "rt_cube_build_device": (ctypes.c_int, [vp, vp, vp, i32, vp, vp, vp]),
         "rt_scene_synthetic_device": (ctypes.c_int, [vp, i32, i32, i32, i32, ctypes.c_uint64,
                                                      f32, vp, vp, vp, vp, vp, vp]),
@@ -418,6 +419,12 @@ class RayTracer:
         """Diagnostics: coarse-list byte budget (0 = default); frames over it
         render as internal row bands."""
         _check(library().rt_debug_set_list_budget(self._ctx, nbytes), "rt_debug_set_list_budget")
+
+    def set_small_path(self, enable: bool) -> None:
+        """Scenes of at most 64 primitives: trace_small_kernel (default) or the
+        general prep -> coarse -> trace path (diagnostics / tests)."""
+        _check(library().rt_debug_set_small_path(self._ctx, int(enable)),
+               "rt_debug_set_small_path")
 
     def set_bin_masks(self, enable: bool) -> None:
         """Diagnostics: coarse binning from the separable bin masks (default)

@@ -1219,6 +1219,101 @@ __global__ void __launch_bounds__(64 * kTraceWaves) RT_TRACE_ATTR trace3_kernel(
 #endif
 }
 
+// Small scenes (at most 64 primitives, one prep chunk): no coarse kernel and
+// no candidate lists.  Each tile wave ANDs its bin row's and bin column's
+// mask words (the chunk's candidates, in primitive order), lets lane i
+// classify candidate i against the tile exactly as coarse3_kernel does, and
+// walks the kept candidates from the ballots.  Saves the coarse launch and
+// one kernel boundary, which dominate small frames (config 2).
+template <int kFmt>
+__global__ void __launch_bounds__(64) RT_TRACE_ATTR trace_small_kernel(
+    const unsigned long long* __restrict__ row_masks,
+    const unsigned long long* __restrict__ col_masks, const int4* __restrict__ boxes,
+    const Cls* __restrict__ cls, const TriRec* __restrict__ tri, const SphRec* __restrict__ sph,
+    const float4* __restrict__ colours, const unsigned* __restrict__ nonfinite_flag,
+    unsigned gen, int n_cubes, int n_cx, int width, int row_begin, int row_end,
+    SceneDev scene, float4 dir, void* __restrict__ out) {
+    const int bid = (int)blockIdx.x;
+    const int cb = bid / kTiles;
+    const int t = __builtin_amdgcn_readfirstlane(bid % kTiles);
+    const int lane = threadIdx.x & 63;
+    const int n_tri = 12 * n_cubes;
+    const int rel_x = (cb % n_cx) * kCoarseW + (t % kTilesX) * kWaveTile;
+    const int rel_y = (cb / n_cx) * kCoarseH + (t / kTilesX) * kWaveTileH;
+    if (!(rel_x < width && rel_y < row_end - row_begin)) return;  // outside: no stores
+    const int tile_x = rel_x, tile_y = row_begin + rel_y;
+    const int x = tile_x + (lane % kWaveTile);
+    const int y0 = tile_y + (lane / kWaveTile);
+    const unsigned long long cand = row_masks[cb / n_cx] & col_masks[cb % n_cx];
+    const bool nonfinite = *nonfinite_flag == gen;
+    int4v pix[kRowsPerLane];
+    if (nonfinite) {  // the reference algorithm verbatim (see trace3_kernel)
+#pragma unroll 1
+        for (int j = 0; j < kRowsPerLane; ++j) {
+            const int y = y0 + kLaneRows * j;
+            if (x < width && y < row_end)
+                store_fmt<kFmt>(out, (int64_t)(y - row_begin) * width + x,
+                                collide_generic(scene, make_float4((float)x, (float)y, 0.0f, 1.0f),
+                                                dir));
+        }
+        return;
+    }
+    // lane i: candidate i against this tile (coarse3_kernel's test)
+    bool keep_l = false, inside_l = false;
+    if ((cand >> lane) & 1ull) {
+        const int4 pb = boxes[lane];
+        const int tx = tile_x, ty = tile_y;
+        if (pb.x <= tx + kWaveTile - 1 && pb.z >= tx && pb.y <= ty + kWaveTileH - 1 &&
+            pb.w >= ty)
+            classify(cls[lane], lane < n_tri, (float)tx, (float)ty, &keep_l, &inside_l);
+    }
+    unsigned long long keep = __ballot(keep_l);
+    const unsigned long long inside = __ballot(keep_l && inside_l);
+    float closest[kRowsPerLane];
+    int hit[kRowsPerLane];
+    double py[kRowsPerLane];
+    float pyf[kRowsPerLane];
+#pragma unroll
+    for (int j = 0; j < kRowsPerLane; ++j) {
+        closest[j] = kFar;
+        hit[j] = -1;
+        py[j] = (double)(y0 + kLaneRows * j);
+        pyf[j] = (float)(y0 + kLaneRows * j);
+    }
+    const double px = (double)x;
+    const float pxf = (float)x;
+#if RT_DEPTH_CULL
+    unsigned tile_max_key = order_key(kFar);
+    bool dirty = false;
+#endif
+    while (keep) {  // kept candidates in primitive order
+        const int p = __builtin_ctzll(keep);
+        keep &= keep - 1ull;
+        const unsigned bits = ((inside >> p) & 1ull) ? kTileMask : kKeepMask;
+        if (p < n_tri) {
+            const TriRec r = tri[p];
+            asm volatile("" ::"s"(r.p0), "s"(r.p1), "s"(r.dz));
+            test_tri(r, p / 12, bits, px, py, closest, hit);
+        } else {
+            const SphRec r = sph[p - n_tri];
+#if RT_DEPTH_CULL
+            if (dirty) {
+                tile_max_key = wave_max_key(closest);
+                dirty = false;
+            }
+            if (r.tmin_key >= tile_max_key) continue;
+#endif
+            test_sph(r, n_cubes + (p - n_tri), bits, pxf, pyf, closest, hit);
+        }
+#if RT_DEPTH_CULL
+        dirty = true;
+#endif
+    }
+    shade_pixels<0>(colours, closest, hit, pix);
+    const bool full = rel_x + kWaveTile <= width && tile_y + kWaveTileH <= row_end;
+    store_rows<0, kFmt>(pix, x, y0, width, row_begin, row_end, full, out);
+}
+
 // fp32 self-test: the device's sqrtf and '/' must be correctly rounded.
 __global__ void fp32_selftest_kernel(const float* in, int n, float* out_sqrt, float* out_div) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1248,6 +1343,7 @@ struct rt_ctx {
     // lists would exceed this is rendered as internal row bands
     int64_t list_budget = (int64_t)4 << 30;
     bool bin_masks = RT_BIN_MASKS != 0;  // separable bin masks (false: coarse scans every box)
+    bool small_path = true;  // <= 64 primitives: trace_small_kernel, no coarse kernel
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     // profiling: per render, start/stop events of the prep, coarse and trace
     // kernels, attached to the kernels' own dispatch packets
@@ -1437,6 +1533,20 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
         ctx->gen = 1;
     }
 
+    if (n_prims > 0 && n_chunks == 1 && use_masks && ctx->small_path && ctx->trace_mode == 0) {
+        rc = launch_k(prep_kernel, dim3(1), dim3(kPrepThreads), stream, pe_prep, sd, dir, width,
+                      row_begin, row_end, tri, sph, boxes, clsv, colours, ctx->flag, ctx->gen,
+                      row_masks, col_masks, n_cx, n_cy);
+        if (rc) return rc;
+        if ((rc = skip_k(stream, pe_coarse))) return rc;
+        auto small = fmt == RT_FORMAT_I32X4 ? trace_small_kernel<RT_FORMAT_I32X4>
+                                            : trace_small_kernel<RT_FORMAT_RGBA8>;
+        return launch_k(small, dim3((unsigned)(n_coarse64 * kTiles)), dim3(64), stream, pe_trace,
+                        (const unsigned long long*)row_masks, (const unsigned long long*)col_masks,
+                        (const int4*)boxes, (const Cls*)clsv, (const TriRec*)tri,
+                        (const SphRec*)sph, (const float4*)colours, (const unsigned*)ctx->flag,
+                        ctx->gen, s->num_cubes, n_cx, width, row_begin, row_end, sd, dir, out);
+    }
     if (n_prims > 0) {
         rc = launch_k(prep_kernel, dim3((unsigned)n_chunks), dim3(kPrepThreads), stream, pe_prep,
                       sd, dir, width, row_begin, row_end, tri, sph, boxes, clsv, colours,
@@ -1705,6 +1815,12 @@ int rt_debug_set_list_budget(rt_ctx* ctx, int64_t bytes) {
 int rt_debug_set_bin_masks(rt_ctx* ctx, int enable) {
     if (!ctx) return RT_ERR_INVALID_ARG;
     ctx->bin_masks = enable != 0;
+    return RT_OK;
+}
+
+int rt_debug_set_small_path(rt_ctx* ctx, int enable) {
+    if (!ctx) return RT_ERR_INVALID_ARG;
+    ctx->small_path = enable != 0;
     return RT_OK;
 }
 

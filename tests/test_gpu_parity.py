@@ -180,10 +180,16 @@ EDGE_CASES = {
 def test_edge_cases(pkg, rt, oracle, case, size):
     w, h = size
     scene = _scene_from(pkg, **EDGE_CASES[case])
-    for path in ("binned", "generic"):
-        got, _ = rt.render(scene, w, h, path=path)
-        want = oracle.trace(scene, w, h)
-        assert not diff_report(got, want), f"{path}: {diff_report(got, want)}"
+    want = oracle.trace(scene, w, h)
+    try:
+        # binned: the small-scene kernel (<= 64 primitives), then the general
+        # prep -> coarse -> trace path on the same scene
+        for path, small in (("binned", True), ("binned", False), ("generic", True)):
+            rt.set_small_path(small)
+            got, _ = rt.render(scene, w, h, path=path)
+            assert not diff_report(got, want), f"{path}/{small}: {diff_report(got, want)}"
+    finally:
+        rt.set_small_path(True)
 
 
 def test_nonfinite_scene_falls_back_exactly(pkg, rt, oracle):
@@ -194,10 +200,47 @@ def test_nonfinite_scene_falls_back_exactly(pkg, rt, oracle):
                         cubes=[([("scale", 10, 10, 10), ("translate", 40, 40, -30)],
                                 (.5, .5, 1, 255))])
     scene.cube_vertices[0, 4, 0] = np.nan
-    got, t = rt.render(scene, 90, 70)
-    assert t.path == "binned"
     want = oracle.trace(scene, 90, 70)
-    assert np.array_equal(got, want)
+    try:
+        for small in (True, False):
+            rt.set_small_path(small)
+            got, t = rt.render(scene, 90, 70)
+            assert t.path == "binned"
+            assert np.array_equal(got, want), small
+    finally:
+        rt.set_small_path(True)
+
+
+@pytest.mark.parametrize("w,h,ns,nc,k", [(512, 512, 4, 1, 1.0), (1920, 1080, 16, 4, 3.0),
+                                         (1000, 777, 40, 2, 2.0), (333, 4100, 64, 0, 2.0),
+                                         (4160, 70, 4, 5, 3.0), (777, 555, 16, 4, 2.5)])
+def test_small_scene_path(pkg, rt, oracle, w, h, ns, nc, k):
+    """<= 64 primitives (one prep chunk): trace_small_kernel classifies each
+    tile's candidates itself.  Same frames as the general path and the oracle,
+    whole frames, row bands and the Texture format; 65 primitives take the
+    general path."""
+    scene = pkg.Scene.synthetic(w, h, ns, nc, seed=w + ns, k=k)
+    assert ns + 12 * nc <= 64
+    frames = {}
+    try:
+        for small in (True, False):
+            rt.set_small_path(small)
+            full, t = rt.render(scene, w, h)
+            assert t.path == "binned"
+            band, _ = rt.render(scene, w, h, rows=(h // 3, h - h // 5))
+            assert np.array_equal(band, full[h // 3:h - h // 5])
+            tex, _ = rt.render(scene, w, h, fmt="rgba8")
+            assert np.array_equal(tex, pkg.pack_rgba8(full))
+            frames[small] = full
+    finally:
+        rt.set_small_path(True)
+    assert np.array_equal(frames[True], frames[False])
+    want = oracle.trace(scene, w, h, threads=THREADS)
+    assert not diff_report(frames[True], want), diff_report(frames[True], want)
+    # one more primitive: the general path
+    big = pkg.Scene.synthetic(w, h, 65 - 12 * nc, nc, seed=w, k=k)
+    got, _ = rt.render(big, w, h)
+    assert np.array_equal(got, oracle.trace(big, w, h, threads=THREADS))
 
 
 def test_deterministic(pkg, rt):
