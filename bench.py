@@ -253,13 +253,19 @@ def main():
                           f" px") + f" of the same scene, oracle/rt_oracle.c orc_trace_rows_mt on "
                          f"{threads} threads, {c_s:.1f} s wall"}
 
+    # BASELINE.json config names, by the per-rank workload
+    names = {(1920, 1080, 16, 4): "config2", (4096, 4096, 256, 64): "config3",
+             (8192, 8192, 192, 64): "config4", (16384, 16384, 4096, 0): "config5"}
+    workload = names.get((w, rows, args.spheres, args.cubes), "custom")
+    # the dominant kernel: scenes of at most 64 primitives take trace_small_kernel
+    kernel = "trace_small_kernel" if 0 < n_sph + 12 * n_cub <= 64 else "trace3_kernel"
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "Mrays/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(wall_ms, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic",
-            "config": {"workload": f"config3: {w}x{rows} rows/rank, {args.spheres} spheres + "
+            "config": {"workload": f"{workload}: {w}x{rows} rows/rank, {args.spheres} spheres + "
                                    f"{args.cubes} cubes per rank, dense k={k:.2f}, seed {args.seed}",
                        "width": w, "rows_per_rank": rows, "image_height": full_h,
                        "spheres": n_sph, "cubes": n_cub, "format": args.format,
@@ -268,7 +274,7 @@ def main():
                                          else "")},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic, "kernel": "trace3_kernel",
+                         "traffic": traffic, "kernel": kernel,
                          "kernel_ms": round(trace_ms, 4), "prep_ms": round(prep_ms, 4),
                          "bin_ms": round(bin_ms, 4), "algo_bytes_per_launch": algo_bytes},
             "event_ms_per_step": round(event_ms, 4),

@@ -1349,6 +1349,7 @@ struct rt_ctx {
     // kernels, attached to the kernels' own dispatch packets
     bool profile = false;
     std::vector<hipEvent_t> prof_events;  // a pool: created once, reused
+    std::vector<unsigned char> prof_skipped;  // per event pair: no kernel ran (0 ms)
     size_t prof_used = 0;                 // events holding this batch's timestamps
     int32_t prof_count = 0;
 };
@@ -1416,11 +1417,12 @@ int launch_k(K kernel, dim3 grid, dim3 block, hipStream_t stream, const hipEvent
     return hipGetLastError() == hipSuccess ? RT_OK : RT_ERR_HIP;
 }
 
-// A profiled kernel slot that runs nothing: both events on the stream.
-int skip_k(hipStream_t stream, const hipEvent_t* ev) {
+// A profiled kernel slot that runs nothing: flagged, so it reads 0 ms.
+// (Recording the two events back to back would time the marker packets
+// themselves, ~5 us, not a kernel.)
+int skip_k(rt_ctx* ctx, const hipEvent_t* ev) {
     if (!ev) return RT_OK;
-    HIP_TRY(hipEventRecord(ev[0], stream));
-    HIP_TRY(hipEventRecord(ev[1], stream));
+    ctx->prof_skipped[(size_t)(ev - ctx->prof_events.data()) / 2] = 1;
     return RT_OK;
 }
 
@@ -1469,6 +1471,8 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
             HIP_TRY(hipEventCreate(&e));
             ctx->prof_events.push_back(e);
         }
+        ctx->prof_skipped.resize(ctx->prof_events.size() / 2);
+        for (int k = 0; k < 3; ++k) ctx->prof_skipped[ctx->prof_used / 2 + k] = 0;
         pe = &ctx->prof_events[ctx->prof_used];
         ctx->prof_used += 6;
         ++ctx->prof_count;
@@ -1480,7 +1484,7 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
     if (!use_bin) {
         const int64_t n = (int64_t)width * rows;
         const int64_t blocks = std::min<int64_t>((n + kThreads - 1) / kThreads, (int64_t)1 << 20);
-        if ((rc = skip_k(stream, pe_prep)) || (rc = skip_k(stream, pe_coarse))) return rc;
+        if ((rc = skip_k(ctx, pe_prep)) || (rc = skip_k(ctx, pe_coarse))) return rc;
         return launch_k(generic_kernel, dim3((unsigned)blocks), dim3(kThreads), stream, pe_trace,
                         sd, dir, reinterpret_cast<const float4*>(origins), width, row_begin,
                         row_end, fmt, out);
@@ -1538,7 +1542,7 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
                       row_begin, row_end, tri, sph, boxes, clsv, colours, ctx->flag, ctx->gen,
                       row_masks, col_masks, n_cx, n_cy);
         if (rc) return rc;
-        if ((rc = skip_k(stream, pe_coarse))) return rc;
+        if ((rc = skip_k(ctx, pe_coarse))) return rc;
         auto small = fmt == RT_FORMAT_I32X4 ? trace_small_kernel<RT_FORMAT_I32X4>
                                             : trace_small_kernel<RT_FORMAT_RGBA8>;
         return launch_k(small, dim3((unsigned)(n_coarse64 * kTiles)), dim3(64), stream, pe_trace,
@@ -1558,9 +1562,9 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
                       row_begin, half_cap, (const unsigned*)ctx->flag, ctx->gen, counts, lists);
         if (rc) return rc;
     } else {
-        if ((rc = skip_k(stream, pe_prep))) return rc;
+        if ((rc = skip_k(ctx, pe_prep))) return rc;
         HIP_TRY(hipMemsetAsync(counts, 0, sizeof(int) * (size_t)n_coarse, stream));
-        if ((rc = skip_k(stream, pe_coarse))) return rc;
+        if ((rc = skip_k(ctx, pe_coarse))) return rc;
     }
     auto kern = fmt == RT_FORMAT_I32X4
                     ? (ctx->trace_mode == 1   ? trace3_kernel<1, RT_FORMAT_I32X4>
@@ -1742,8 +1746,13 @@ int rt_profile_read(rt_ctx* ctx, double* prep_ms, double* bin_ms, double* trace_
     HIP_TRY(hipSetDevice(ctx->device));
     double sums[3] = {0, 0, 0};
     for (size_t q = 0; q + 5 < ctx->prof_used; q += 6) {
-        HIP_TRY(hipEventSynchronize(ctx->prof_events[q + 5]));
+        for (int k = 2; k >= 0; --k)  // the last kernel that ran
+            if (!ctx->prof_skipped[q / 2 + k]) {
+                HIP_TRY(hipEventSynchronize(ctx->prof_events[q + 2 * k + 1]));
+                break;
+            }
         for (int k = 0; k < 3; ++k) {
+            if (ctx->prof_skipped[q / 2 + k]) continue;
             float ms = 0.0f;
             HIP_TRY(hipEventElapsedTime(&ms, ctx->prof_events[q + 2 * k],
                                         ctx->prof_events[q + 2 * k + 1]));

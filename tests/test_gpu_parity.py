@@ -573,3 +573,26 @@ def test_list_budget_bands(pkg, rt, oracle):
         rt.set_list_budget(0)
     want = oracle.trace(scene, w, h, threads=THREADS)
     assert not diff_report(full, want), diff_report(full, want)
+
+
+def test_profile_slots_of_skipped_kernels(pkg, rt):
+    """Per-kernel profiling: a kernel that does not run reads 0 ms (small
+    scenes skip the coarse kernel, empty scenes prep and coarse, the generic
+    path both), the kernels that run read > 0."""
+    small = pkg.Scene.synthetic(640, 480, 8, 2, seed=2, k=1.0)
+    big = pkg.Scene.synthetic(640, 480, 100, 10, seed=2, k=1.0)
+    cases = [(small, "binned", (True, False, True)), (big, "binned", (True, True, True)),
+             (pkg.Scene(), "binned", (False, False, True)),
+             (small, "generic", (False, False, True))]
+    try:
+        for scene, path, ran in cases:
+            rt.profile(True)
+            rt.render(scene, 640, 480, path=path)
+            rt.render(scene, 640, 480, path=path)
+            prof = rt.profile_read()
+            rt.profile(False)
+            assert prof["renders"] == 2, prof
+            for key, on in zip(("prep_ms", "bin_ms", "trace_ms"), ran):
+                assert (prof[key] > 0) == on, (path, key, prof)
+    finally:
+        rt.profile(False)
