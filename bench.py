@@ -216,6 +216,27 @@ def main():
                   "bytes_to_root": algo_bytes * (world - 1),
                   "render_plus_gather_mrays": round(
                       world * rays_rank / ((wall_ms + g_ms) * 1e-3) / 1e6, 1)}
+        if args.format == "i32x4":
+            # The Texture assembly: the same bands rendered in
+            # the Texture's RGBA8 packing (MainState.cpp:1023-1037) gather 4x
+            # fewer bytes.  Rendered once, untimed; the gather is timed alone.
+            tex = torch.empty((rows, w), dtype=torch.int32, device=dev)
+            rt.bind_render_device(dscene, w, full_h, (rb, re), tex.data_ptr(), fmt="rgba8",
+                                  stream=stream.cuda_stream)()
+            torch.cuda.synchronize(dev)
+            tband = tex if coll_dev == dev else tex.cpu()
+            for _ in range(2):
+                rowbands.gather_frame(tband, full_h, world, rank)
+            torch.cuda.synchronize(dev)
+            barrier()
+            g0 = time.perf_counter()
+            for _ in range(reps):
+                rowbands.gather_frame(tband, full_h, world, rank)
+            torch.cuda.synchronize(dev)
+            barrier()
+            t_ms = (time.perf_counter() - g0) * 1e3 / reps
+            gather["texture_rgba8"] = {"ms": round(t_ms, 4),
+                                       "bytes_to_root": 4 * rays_rank * (world - 1)}
 
     host = None
     if world == 1 and not args.no_host_path:
