@@ -1219,19 +1219,23 @@ __global__ void __launch_bounds__(64 * kTraceWaves) RT_TRACE_ATTR trace3_kernel(
 #endif
 }
 
-// Small scenes (at most 64 primitives, one prep chunk): no coarse kernel and
-// no candidate lists.  Each tile wave ANDs its bin row's and bin column's
-// mask words (the chunk's candidates, in primitive order), lets lane i
-// classify candidate i against the tile exactly as coarse3_kernel does, and
-// walks the kept candidates from the ballots.  Saves the coarse launch and
+// Small scenes (at most 64 x RT_SMALL_CHUNKS primitives, that many prep
+// chunks): no coarse kernel and no candidate lists.  Each tile wave ANDs its
+// bin row's and bin column's mask words per chunk (the candidates, in
+// primitive order), lets lane i classify candidate 64 c + i against the tile
+// exactly as coarse3_kernel does, and walks the kept candidates from the
+// ballots, chunk by chunk.  Saves the coarse launch and
 // one kernel boundary, which dominate small frames (config 2).
-template <int kFmt>
+#ifndef RT_SMALL_CHUNKS
+#define RT_SMALL_CHUNKS 4  // the small-scene path takes scenes of up to 64 x this many primitives
+#endif
+template <int kFmt, int kChunks>
 __global__ void __launch_bounds__(64) RT_TRACE_ATTR trace_small_kernel(
     const unsigned long long* __restrict__ row_masks,
     const unsigned long long* __restrict__ col_masks, const int4* __restrict__ boxes,
     const Cls* __restrict__ cls, const TriRec* __restrict__ tri, const SphRec* __restrict__ sph,
     const float4* __restrict__ colours, const unsigned* __restrict__ nonfinite_flag,
-    unsigned gen, int n_cubes, int n_cx, int width, int row_begin, int row_end,
+    unsigned gen, int n_cubes, int n_cx, int n_chunks, int width, int row_begin, int row_end,
     SceneDev scene, float4 dir, void* __restrict__ out) {
     const int bid = (int)blockIdx.x;
     const int cb = bid / kTiles;
@@ -1244,7 +1248,12 @@ __global__ void __launch_bounds__(64) RT_TRACE_ATTR trace_small_kernel(
     const int tile_x = rel_x, tile_y = row_begin + rel_y;
     const int x = tile_x + (lane % kWaveTile);
     const int y0 = tile_y + (lane / kWaveTile);
-    const unsigned long long cand = row_masks[cb / n_cx] & col_masks[cb % n_cx];
+    unsigned long long cand[kChunks];
+#pragma unroll
+    for (int c = 0; c < kChunks; ++c)
+        cand[c] = c < n_chunks ? row_masks[(int64_t)(cb / n_cx) * n_chunks + c] &
+                                     col_masks[(int64_t)(cb % n_cx) * n_chunks + c]
+                               : 0ull;
     const bool nonfinite = *nonfinite_flag == gen;
     int4v pix[kRowsPerLane];
     if (nonfinite) {  // the reference algorithm verbatim (see trace3_kernel)
@@ -1258,17 +1267,22 @@ __global__ void __launch_bounds__(64) RT_TRACE_ATTR trace_small_kernel(
         }
         return;
     }
-    // lane i: candidate i against this tile (coarse3_kernel's test)
-    bool keep_l = false, inside_l = false;
-    if ((cand >> lane) & 1ull) {
-        const int4 pb = boxes[lane];
-        const int tx = tile_x, ty = tile_y;
-        if (pb.x <= tx + kWaveTile - 1 && pb.z >= tx && pb.y <= ty + kWaveTileH - 1 &&
-            pb.w >= ty)
-            classify(cls[lane], lane < n_tri, (float)tx, (float)ty, &keep_l, &inside_l);
+    // lane i: candidate 64 c + i against this tile (coarse3_kernel's test)
+    unsigned long long keep[kChunks], inside[kChunks];
+#pragma unroll
+    for (int c = 0; c < kChunks; ++c) {
+        const int q = 64 * c + lane;
+        bool keep_l = false, inside_l = false;
+        if ((cand[c] >> lane) & 1ull) {
+            const int4 pb = boxes[q];
+            const int tx = tile_x, ty = tile_y;
+            if (pb.x <= tx + kWaveTile - 1 && pb.z >= tx && pb.y <= ty + kWaveTileH - 1 &&
+                pb.w >= ty)
+                classify(cls[q], q < n_tri, (float)tx, (float)ty, &keep_l, &inside_l);
+        }
+        keep[c] = __ballot(keep_l);
+        inside[c] = __ballot(keep_l && inside_l);
     }
-    unsigned long long keep = __ballot(keep_l);
-    const unsigned long long inside = __ballot(keep_l && inside_l);
     float closest[kRowsPerLane];
     int hit[kRowsPerLane];
     double py[kRowsPerLane];
@@ -1286,10 +1300,13 @@ __global__ void __launch_bounds__(64) RT_TRACE_ATTR trace_small_kernel(
     unsigned tile_max_key = order_key(kFar);
     bool dirty = false;
 #endif
-    while (keep) {  // kept candidates in primitive order
-        const int p = __builtin_ctzll(keep);
-        keep &= keep - 1ull;
-        const unsigned bits = ((inside >> p) & 1ull) ? kTileMask : kKeepMask;
+#pragma unroll
+    for (int c = 0; c < kChunks; ++c)
+    while (keep[c]) {  // kept candidates in primitive order
+        const int b = __builtin_ctzll(keep[c]);
+        keep[c] &= keep[c] - 1ull;
+        const int p = 64 * c + b;
+        const unsigned bits = ((inside[c] >> b) & 1ull) ? kTileMask : kKeepMask;
         if (p < n_tri) {
             const TriRec r = tri[p];
             asm volatile("" ::"s"(r.p0), "s"(r.p1), "s"(r.dz));
@@ -1343,7 +1360,7 @@ struct rt_ctx {
     // lists would exceed this is rendered as internal row bands
     int64_t list_budget = (int64_t)4 << 30;
     bool bin_masks = RT_BIN_MASKS != 0;  // separable bin masks (false: coarse scans every box)
-    bool small_path = true;  // <= 64 primitives: trace_small_kernel, no coarse kernel
+    bool small_path = true;  // <= 64 x RT_SMALL_CHUNKS primitives: trace_small_kernel
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     // profiling: per render, start/stop events of the prep, coarse and trace
     // kernels, attached to the kernels' own dispatch packets
@@ -1537,19 +1554,25 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
         ctx->gen = 1;
     }
 
-    if (n_prims > 0 && n_chunks == 1 && use_masks && ctx->small_path && ctx->trace_mode == 0) {
-        rc = launch_k(prep_kernel, dim3(1), dim3(kPrepThreads), stream, pe_prep, sd, dir, width,
+    if (n_prims > 0 && n_chunks <= RT_SMALL_CHUNKS && use_masks && ctx->small_path &&
+        ctx->trace_mode == 0) {
+        rc = launch_k(prep_kernel, dim3((unsigned)n_chunks), dim3(kPrepThreads), stream, pe_prep, sd, dir, width,
                       row_begin, row_end, tri, sph, boxes, clsv, colours, ctx->flag, ctx->gen,
                       row_masks, col_masks, n_cx, n_cy);
         if (rc) return rc;
         if ((rc = skip_k(ctx, pe_coarse))) return rc;
-        auto small = fmt == RT_FORMAT_I32X4 ? trace_small_kernel<RT_FORMAT_I32X4>
-                                            : trace_small_kernel<RT_FORMAT_RGBA8>;
+        auto small = n_chunks == 1
+                         ? (fmt == RT_FORMAT_I32X4 ? trace_small_kernel<RT_FORMAT_I32X4, 1>
+                                                   : trace_small_kernel<RT_FORMAT_RGBA8, 1>)
+                         : (fmt == RT_FORMAT_I32X4
+                                ? trace_small_kernel<RT_FORMAT_I32X4, RT_SMALL_CHUNKS>
+                                : trace_small_kernel<RT_FORMAT_RGBA8, RT_SMALL_CHUNKS>);
         return launch_k(small, dim3((unsigned)(n_coarse64 * kTiles)), dim3(64), stream, pe_trace,
                         (const unsigned long long*)row_masks, (const unsigned long long*)col_masks,
                         (const int4*)boxes, (const Cls*)clsv, (const TriRec*)tri,
                         (const SphRec*)sph, (const float4*)colours, (const unsigned*)ctx->flag,
-                        ctx->gen, s->num_cubes, n_cx, width, row_begin, row_end, sd, dir, out);
+                        ctx->gen, s->num_cubes, n_cx, n_chunks, width, row_begin, row_end, sd,
+                        dir, out);
     }
     if (n_prims > 0) {
         rc = launch_k(prep_kernel, dim3((unsigned)n_chunks), dim3(kPrepThreads), stream, pe_prep,

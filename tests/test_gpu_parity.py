@@ -182,7 +182,7 @@ def test_edge_cases(pkg, rt, oracle, case, size):
     scene = _scene_from(pkg, **EDGE_CASES[case])
     want = oracle.trace(scene, w, h)
     try:
-        # binned: the small-scene kernel (<= 64 primitives), then the general
+        # binned: the small-scene kernel (<= 256 primitives), then the general
         # prep -> coarse -> trace path on the same scene
         for path, small in (("binned", True), ("binned", False), ("generic", True)):
             rt.set_small_path(small)
@@ -213,14 +213,17 @@ def test_nonfinite_scene_falls_back_exactly(pkg, rt, oracle):
 
 @pytest.mark.parametrize("w,h,ns,nc,k", [(512, 512, 4, 1, 1.0), (1920, 1080, 16, 4, 3.0),
                                          (1000, 777, 40, 2, 2.0), (333, 4100, 64, 0, 2.0),
-                                         (4160, 70, 4, 5, 3.0), (777, 555, 16, 4, 2.5)])
+                                         (4160, 70, 4, 5, 3.0), (777, 555, 16, 4, 2.5),
+                                         (640, 480, 8, 10, 1.0), (1920, 1080, 32, 8, 3.0),
+                                         (1500, 900, 65, 0, 2.0), (1920, 1080, 64, 16, 3.0),
+                                         (2000, 1300, 100, 13, 2.0)])
 def test_small_scene_path(pkg, rt, oracle, w, h, ns, nc, k):
-    """<= 64 primitives (one prep chunk): trace_small_kernel classifies each
-    tile's candidates itself.  Same frames as the general path and the oracle,
-    whole frames, row bands and the Texture format; 65 primitives take the
-    general path."""
+    """<= 256 primitives (up to 4 prep chunks): trace_small_kernel classifies
+    each tile's candidates itself.  Same frames as the general path and the
+    oracle, whole frames, row bands and the Texture format; 257 primitives
+    take the general path."""
     scene = pkg.Scene.synthetic(w, h, ns, nc, seed=w + ns, k=k)
-    assert ns + 12 * nc <= 64
+    assert ns + 12 * nc <= 256
     frames = {}
     try:
         for small in (True, False):
@@ -238,7 +241,7 @@ def test_small_scene_path(pkg, rt, oracle, w, h, ns, nc, k):
     want = oracle.trace(scene, w, h, threads=THREADS)
     assert not diff_report(frames[True], want), diff_report(frames[True], want)
     # one more primitive: the general path
-    big = pkg.Scene.synthetic(w, h, 65 - 12 * nc, nc, seed=w, k=k)
+    big = pkg.Scene.synthetic(w, h, 257 - 12 * nc, nc, seed=w, k=k)
     got, _ = rt.render(big, w, h)
     assert np.array_equal(got, oracle.trace(big, w, h, threads=THREADS))
 
@@ -580,7 +583,7 @@ def test_profile_slots_of_skipped_kernels(pkg, rt):
     scenes skip the coarse kernel, empty scenes prep and coarse, the generic
     path both), the kernels that run read > 0."""
     small = pkg.Scene.synthetic(640, 480, 8, 2, seed=2, k=1.0)
-    big = pkg.Scene.synthetic(640, 480, 100, 10, seed=2, k=1.0)
+    big = pkg.Scene.synthetic(640, 480, 300, 10, seed=2, k=1.0)
     cases = [(small, "binned", (True, False, True)), (big, "binned", (True, True, True)),
              (pkg.Scene(), "binned", (False, False, True)),
              (small, "generic", (False, False, True))]
