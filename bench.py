@@ -278,8 +278,8 @@ def main():
     names = {(1920, 1080, 16, 4): "config2", (4096, 4096, 256, 64): "config3",
              (8192, 8192, 192, 64): "config4", (16384, 16384, 4096, 0): "config5"}
     workload = names.get((w, rows, args.spheres, args.cubes), "custom")
-    # the dominant kernel: scenes of at most 256 primitives take trace_small_kernel
-    kernel = "trace_small_kernel" if 0 < n_sph + 12 * n_cub <= 256 else "trace3_kernel"
+    # the dominant kernel: scenes of at most 512 primitives take trace_small_kernel
+    kernel = "trace_small_kernel" if 0 < n_sph + 12 * n_cub <= 512 else "trace3_kernel"
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "Mrays/s", "n_gpus": world,

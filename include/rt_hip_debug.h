@@ -59,7 +59,7 @@ int rt_debug_set_list_budget(rt_ctx* ctx, int64_t bytes);
  * more than 4096 bin rows + columns take). */
 int rt_debug_set_bin_masks(rt_ctx* ctx, int enable);
 
-/* Scenes of at most 256 primitives: 1 (default) = trace_small_kernel (each
+/* Scenes of at most 512 primitives: 1 (default) = trace_small_kernel (each
  * tile wave classifies its candidates itself, no coarse kernel), 0 = the
  * general prep -> coarse -> trace path. */
 int rt_debug_set_small_path(rt_ctx* ctx, int enable);

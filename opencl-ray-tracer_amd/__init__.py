@@ -421,7 +421,7 @@ class RayTracer:
         _check(library().rt_debug_set_list_budget(self._ctx, nbytes), "rt_debug_set_list_budget")
 
     def set_small_path(self, enable: bool) -> None:
-        """Scenes of at most 256 primitives: trace_small_kernel (default) or the
+        """Scenes of at most 512 primitives: trace_small_kernel (default) or the
         general prep -> coarse -> trace path (diagnostics / tests)."""
         _check(library().rt_debug_set_small_path(self._ctx, int(enable)),
                "rt_debug_set_small_path")

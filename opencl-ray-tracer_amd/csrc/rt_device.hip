@@ -1227,7 +1227,7 @@ __global__ void __launch_bounds__(64 * kTraceWaves) RT_TRACE_ATTR trace3_kernel(
 // ballots, chunk by chunk.  Saves the coarse launch and
 // one kernel boundary, which dominate small frames (config 2).
 #ifndef RT_SMALL_CHUNKS
-#define RT_SMALL_CHUNKS 4  // the small-scene path takes scenes of up to 64 x this many primitives
+#define RT_SMALL_CHUNKS 8  // the small-scene path takes scenes of up to 64 x this many primitives
 #endif
 template <int kFmt, int kChunks>
 __global__ void __launch_bounds__(64) RT_TRACE_ATTR trace_small_kernel(
@@ -1561,11 +1561,16 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
                       row_masks, col_masks, n_cx, n_cy);
         if (rc) return rc;
         if ((rc = skip_k(ctx, pe_coarse))) return rc;
-        auto small = n_chunks == 1
-                         ? (fmt == RT_FORMAT_I32X4 ? trace_small_kernel<RT_FORMAT_I32X4, 1>
-                                                   : trace_small_kernel<RT_FORMAT_RGBA8, 1>)
-                         : (fmt == RT_FORMAT_I32X4
-                                ? trace_small_kernel<RT_FORMAT_I32X4, RT_SMALL_CHUNKS>
+        // the instance with the fewest chunk slots that holds n_chunks
+        const bool i32 = fmt == RT_FORMAT_I32X4;
+        auto small = n_chunks == 1   ? (i32 ? trace_small_kernel<RT_FORMAT_I32X4, 1>
+                                            : trace_small_kernel<RT_FORMAT_RGBA8, 1>)
+                     : n_chunks == 2 ? (i32 ? trace_small_kernel<RT_FORMAT_I32X4, 2>
+                                            : trace_small_kernel<RT_FORMAT_RGBA8, 2>)
+                     : n_chunks <= 4 || RT_SMALL_CHUNKS <= 4
+                         ? (i32 ? trace_small_kernel<RT_FORMAT_I32X4, 4>
+                                : trace_small_kernel<RT_FORMAT_RGBA8, 4>)
+                         : (i32 ? trace_small_kernel<RT_FORMAT_I32X4, RT_SMALL_CHUNKS>
                                 : trace_small_kernel<RT_FORMAT_RGBA8, RT_SMALL_CHUNKS>);
         return launch_k(small, dim3((unsigned)(n_coarse64 * kTiles)), dim3(64), stream, pe_trace,
                         (const unsigned long long*)row_masks, (const unsigned long long*)col_masks,

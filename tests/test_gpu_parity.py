@@ -182,7 +182,7 @@ def test_edge_cases(pkg, rt, oracle, case, size):
     scene = _scene_from(pkg, **EDGE_CASES[case])
     want = oracle.trace(scene, w, h)
     try:
-        # binned: the small-scene kernel (<= 256 primitives), then the general
+        # binned: the small-scene kernel (<= 512 primitives), then the general
         # prep -> coarse -> trace path on the same scene
         for path, small in (("binned", True), ("binned", False), ("generic", True)):
             rt.set_small_path(small)
@@ -216,14 +216,15 @@ def test_nonfinite_scene_falls_back_exactly(pkg, rt, oracle):
                                          (4160, 70, 4, 5, 3.0), (777, 555, 16, 4, 2.5),
                                          (640, 480, 8, 10, 1.0), (1920, 1080, 32, 8, 3.0),
                                          (1500, 900, 65, 0, 2.0), (1920, 1080, 64, 16, 3.0),
-                                         (2000, 1300, 100, 13, 2.0)])
+                                         (2000, 1300, 100, 13, 2.0), (1920, 1080, 128, 32, 3.0),
+                                         (1111, 999, 300, 10, 2.0), (3000, 700, 512, 0, 3.0)])
 def test_small_scene_path(pkg, rt, oracle, w, h, ns, nc, k):
-    """<= 256 primitives (up to 4 prep chunks): trace_small_kernel classifies
+    """<= 512 primitives (up to 8 prep chunks): trace_small_kernel classifies
     each tile's candidates itself.  Same frames as the general path and the
-    oracle, whole frames, row bands and the Texture format; 257 primitives
+    oracle, whole frames, row bands and the Texture format; 513 primitives
     take the general path."""
     scene = pkg.Scene.synthetic(w, h, ns, nc, seed=w + ns, k=k)
-    assert ns + 12 * nc <= 256
+    assert ns + 12 * nc <= 512
     frames = {}
     try:
         for small in (True, False):
@@ -241,7 +242,7 @@ def test_small_scene_path(pkg, rt, oracle, w, h, ns, nc, k):
     want = oracle.trace(scene, w, h, threads=THREADS)
     assert not diff_report(frames[True], want), diff_report(frames[True], want)
     # one more primitive: the general path
-    big = pkg.Scene.synthetic(w, h, 257 - 12 * nc, nc, seed=w, k=k)
+    big = pkg.Scene.synthetic(w, h, 513 - 12 * nc, nc, seed=w, k=k)
     got, _ = rt.render(big, w, h)
     assert np.array_equal(got, oracle.trace(big, w, h, threads=THREADS))
 
@@ -583,7 +584,7 @@ def test_profile_slots_of_skipped_kernels(pkg, rt):
     scenes skip the coarse kernel, empty scenes prep and coarse, the generic
     path both), the kernels that run read > 0."""
     small = pkg.Scene.synthetic(640, 480, 8, 2, seed=2, k=1.0)
-    big = pkg.Scene.synthetic(640, 480, 300, 10, seed=2, k=1.0)
+    big = pkg.Scene.synthetic(640, 480, 500, 10, seed=2, k=1.0)
     cases = [(small, "binned", (True, False, True)), (big, "binned", (True, True, True)),
              (pkg.Scene(), "binned", (False, False, True)),
              (small, "generic", (False, False, True))]
