@@ -7,7 +7,8 @@
 // fp64 Moller-Trumbore for cube triangles, fp32 glm sphere test, strict '<'
 // closest hit in cubes-then-spheres order, depth-ramp shade, (int) stores.
 //
-// Three kernels per frame (DESIGN.md "Kernels"):
+// Three kernels per frame (DESIGN.md "Kernels"; scenes of at most 512
+// primitives use two: prep, then trace_small_kernel, which bins its own tile):
 //   prep   one lane per primitive: per-triangle fp64 constants, per-sphere
 //          fp32 constants, and a conservative integer pixel box outside of
 //          which the exact test provably rejects.
