@@ -9,7 +9,13 @@
 //
 //   rt_headless [--scene 1|2|3] [--seed S] [--width W] [--height H]
 //               [--synthetic N M k] [--rows A B] [--ppm out.ppm] [--repeat R]
-//               [--bands B] [--devices D]
+//               [--bands B] [--devices D] [--device-scene]
+//
+// --device-scene (with --synthetic, one band) builds the scene on the GPU
+// with rt_scene_synthetic_device, renders it with
+// rt_render_device from the device arrays and reads the frame back: no host
+// scene build and no scene upload.  The printed hash must equal the host
+// build's.
 //
 // --bands splits [A, B) into B row bands traced concurrently, one host
 // thread and one rt_ctx per band on device (band % D), each writing its rows
@@ -22,6 +28,8 @@
 #include <string>
 #include <thread>
 #include <vector>
+
+#include <hip/hip_runtime_api.h>
 
 #include "rt_hip.h"
 
@@ -58,6 +66,46 @@ struct Band {
     int status = RT_OK;
 };
 
+// --device-scene: the scene built and rendered on the device, frame read back.
+int render_device_scene(Band& band, int width, int height, int row_begin, int row_end, int n,
+                        int m, unsigned seed, float k, const float ray_dir[4],
+                        std::vector<int32_t>& pixels) {
+    float *so = nullptr, *sr = nullptr, *sc = nullptr, *cv = nullptr, *cc = nullptr;
+    int32_t* out = nullptr;
+    const size_t n4 = 4 * sizeof(float) * (size_t)(n > 0 ? n : 1);
+    const size_t m4 = 4 * sizeof(float) * (size_t)(m > 0 ? m : 1);
+    int status = 1;
+    if (hipMalloc(&so, n4) == hipSuccess && hipMalloc(&sr, n4 / 4) == hipSuccess &&
+        hipMalloc(&sc, n4) == hipSuccess && hipMalloc(&cv, 36 * m4) == hipSuccess &&
+        hipMalloc(&cc, m4) == hipSuccess &&
+        hipMalloc(&out, pixels.size() * sizeof(int32_t)) == hipSuccess) {
+        int rc = rt_scene_synthetic_device(band.ctx, width, height, n, m, seed, k, so, sr, sc,
+                                           cv, cc, nullptr);
+        rt_scene scene{so, sr, sc, n, cv, cc, m, nullptr, 0};
+        if (rc == RT_OK)
+            rc = rt_render_device(band.ctx, &scene, ray_dir, nullptr, width, height, row_begin,
+                                  row_end, RT_FORMAT_I32X4, RT_PATH_AUTO, out, nullptr);
+        if (rc == RT_OK && hipDeviceSynchronize() == hipSuccess &&
+            hipMemcpy(pixels.data(), out, pixels.size() * sizeof(int32_t),
+                      hipMemcpyDeviceToHost) == hipSuccess) {
+            std::printf("device scene: %d spheres, %d cubes built and rendered on the GPU\n",
+                        n, m);
+            std::printf("frame %dx%d rows [%d,%d) spheres %d cubes %d fnv1a64 %016llx\n",
+                        width, height, row_begin, row_end, n, m,
+                        (unsigned long long)fnv1a(pixels.data(), pixels.size()));
+            status = 0;
+        } else {
+            std::fprintf(stderr, "device scene render failed: %s\n", rt_error_string(rc));
+        }
+    } else {
+        std::fprintf(stderr, "hipMalloc failed\n");
+    }
+    for (void* p : {(void*)so, (void*)sr, (void*)sc, (void*)cv, (void*)cc, (void*)out})
+        if (p) (void)hipFree(p);
+    rt_destroy(band.ctx);
+    return status;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -67,6 +115,7 @@ int main(int argc, char** argv) {
     float syn_k = 1.0f;
     int row_begin = 0, row_end = -1;
     int n_bands = 1, n_devices = 1;
+    bool device_scene = false;
     std::string ppm;
     for (int i = 1; i < argc; ++i) {
         std::string a = argv[i];
@@ -92,6 +141,7 @@ int main(int argc, char** argv) {
         else if (a == "--repeat") repeat = std::atoi(next());
         else if (a == "--bands") n_bands = std::atoi(next());
         else if (a == "--devices") n_devices = std::atoi(next());
+        else if (a == "--device-scene") device_scene = true;
         else {
             std::fprintf(stderr, "unknown option %s\n", a.c_str());
             return 2;
@@ -101,6 +151,10 @@ int main(int argc, char** argv) {
     if (n_bands < 1 || n_devices < 1 || row_begin < 0 || row_end > height ||
         row_begin >= row_end) {
         std::fprintf(stderr, "bad --rows/--bands/--devices\n");
+        return 2;
+    }
+    if (device_scene && (syn_n < 0 || n_bands != 1)) {
+        std::fprintf(stderr, "--device-scene needs --synthetic and one band\n");
         return 2;
     }
 
@@ -144,6 +198,8 @@ int main(int argc, char** argv) {
     rt_primary_ray_dir(ray_dir);  // (0,0,-1,-1), MainState.cpp:37-39
     rt_scene scene{so.data(), sr.data(), sc.data(), ns, cv.data(), cc.data(), nc, nullptr, 0};
     std::vector<int32_t> pixels(4 * (size_t)width * rows);
+    if (device_scene) return render_device_scene(bands[0], width, height, row_begin, row_end,
+                                                 syn_n, syn_m, seed, syn_k, ray_dir, pixels);
     auto trace_band = [&](Band& band) {
         int32_t* dst = pixels.data() + 4 * (size_t)width * (band.row_begin - row_begin);
         band.status = rt_render(band.ctx, &scene, ray_dir, nullptr, width, height,

@@ -370,6 +370,35 @@ def test_headless_cpp_driver(pkg, scene_id, tmp_path):
     assert np.array_equal(rgb, g["frame"][..., :3].astype(np.uint8))
 
 
+@pytest.mark.parametrize("args", [["--synthetic", "256", "64", "6.4", "--width", "1024",
+                                   "--height", "768"],
+                                  ["--synthetic", "40", "5", "2", "--width", "999",
+                                   "--height", "333", "--rows", "17", "300"],
+                                  ["--synthetic", "0", "0", "1", "--width", "64",
+                                   "--height", "64"]])
+def test_headless_cpp_driver_device_scene(pkg, args):
+    """The C++ host building the synthetic scene on the device
+    (rt_scene_synthetic_device) and rendering from the device arrays prints
+    the same frame hash as with the host-built scene (whose frames the
+    oracle checks in the tests above)."""
+    import re
+    import subprocess
+
+    exe = Path(pkg.library_path()).parent / "rt_headless"
+    if not exe.exists():
+        pytest.skip("rt_headless not built")
+    env = dict(os.environ)
+    env["LD_LIBRARY_PATH"] = str(exe.parent) + ":" + env.get("LD_LIBRARY_PATH", "")
+    hashes = []
+    for extra in ([], ["--device-scene"]):
+        r = subprocess.run([str(exe), "--seed", "9"] + args + extra, capture_output=True,
+                           text=True, env=env, timeout=120)
+        assert r.returncode == 0, r.stderr
+        hashes.append(re.search(r"fnv1a64 ([0-9a-f]{16})", r.stdout).group(1))
+    assert "device scene" in r.stdout
+    assert hashes[0] == hashes[1]
+
+
 @pytest.mark.parametrize("bands", [3, 7])
 def test_headless_cpp_driver_bands(pkg, bands, tmp_path):
     """rt_headless --bands: concurrent host threads, one rt_ctx each
