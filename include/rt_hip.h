@@ -111,6 +111,21 @@ int rt_render_path(rt_ctx* ctx, const rt_scene* scene, const float ray_dir[4],
                    int32_t row_begin, int32_t row_end, int32_t out_format,
                    int32_t path, void* host_out, rt_timing* timing);
 
+/* In-process multi-GPU render (SURVEY.md §8b/§8e rt_render_multi; the
+ * reference is single-device, MainState.cpp:1241-1266).  Rows
+ * [row_begin, row_end) are split into num_ctx contiguous bands of whole rows
+ * (sizes differ by at most one row); band i is rendered on ctxs[i] (one
+ * context per device, e.g. rt_init(i)) from its own host thread, straight
+ * into its rows of host_out, so no gather step exists: the bands are
+ * disjoint slices of the row-major frame (MainState.cpp:676 `pixels`).
+ * Synchronous.  timings, if not NULL, gets one rt_timing per context
+ * (zeroed for contexts left idle when num_ctx exceeds the row count).
+ * Returns the first failing band's status. */
+int rt_render_multi(rt_ctx* const* ctxs, int32_t num_ctx, const rt_scene* scene,
+                    const float ray_dir[4], const float* ray_origins, int32_t width,
+                    int32_t height, int32_t row_begin, int32_t row_end,
+                    int32_t out_format, void* host_out, rt_timing* timings);
+
 /* Device-resident variant (no reference counterpart; used by the multi-GPU
  * row-band driver and the benchmark): every pointer in `device_scene`,
  * `device_ray_origins` and `device_out` is a device pointer on the context's

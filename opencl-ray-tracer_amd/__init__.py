@@ -24,7 +24,7 @@ __all__ = [
     "RT_ERR_UNSUPPORTED", "RT_FORMAT_I32X4", "RT_FORMAT_RGBA8", "RT_PATH_AUTO", "RT_PATH_BINNED",
     "RT_PATH_GENERIC", "RtError", "Scene", "Timing", "RayTracer", "MainState",
     "library", "library_path", "primary_ray_dir", "pack_rgba8", "cube_packed",
-    "deg_to_rad", "encode_png", "EXPORTED_SYMBOLS", "CUBE_OP_DTYPE", "cube_ops",
+    "deg_to_rad", "encode_png", "EXPORTED_SYMBOLS", "CUBE_OP_DTYPE", "cube_ops", "render_multi",
     "debug_glibc_sincosf",
 ]
 
@@ -44,6 +44,7 @@ EXPORTED_SYMBOLS = (
     "rt_cube_init", "rt_cube_scale", "rt_cube_rotate", "rt_cube_translate",
     "rt_deg_to_rad", "rt_primary_ray_dir", "rt_scene_reference", "rt_scene_synthetic",
     "rt_pack_rgba8", "rt_abi_version", "rt_cube_build_device", "rt_scene_synthetic_device",
+    "rt_render_multi",
 )
 
 
@@ -109,6 +110,9 @@ def library() -> ctypes.CDLL:
                                           i32, i32, i32, vp, ctypes.POINTER(_Timing)]),
         "rt_render_device": (ctypes.c_int, [vp, ctypes.POINTER(_Scene), vp, vp, i32, i32, i32,
                                             i32, i32, i32, vp, vp]),
+        "rt_render_multi": (ctypes.c_int, [ctypes.POINTER(vp), i32, ctypes.POINTER(_Scene), vp,
+                                           vp, i32, i32, i32, i32, i32, vp,
+                                           ctypes.POINTER(_Timing)]),
         "rt_profile_enable": (ctypes.c_int, [vp, ctypes.c_int]),
         "rt_profile_read": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double),
                                            ctypes.POINTER(ctypes.c_double),
@@ -301,6 +305,29 @@ class Timing:
     kernel_us: float
     download_us: float
     path: str
+
+
+def render_multi(tracers, scene: Scene, width: int, height: int,
+                 rows: Optional[Tuple[int, int]] = None, ray_dir: Optional[np.ndarray] = None,
+                 ray_origins: Optional[np.ndarray] = None,
+                 fmt: str = "i32x4") -> Tuple[np.ndarray, list]:
+    """rt_render_multi: one frame (or row range) split into contiguous row
+    bands over `tracers` (one RayTracer per device), rendered concurrently
+    into one host frame.  Returns (frame, per-band Timing list)."""
+    rb, re = rows if rows is not None else (0, height)
+    d = primary_ray_dir() if ray_dir is None else np.ascontiguousarray(ray_dir, np.float32)
+    org = None if ray_origins is None else np.ascontiguousarray(ray_origins, np.float32)
+    shape = (re - rb, width, 4) if fmt == "i32x4" else (re - rb, width)
+    out = np.empty(shape, np.int32 if fmt == "i32x4" else np.uint32)
+    ctxs = (ctypes.c_void_p * len(tracers))(*[t.handle.value for t in tracers])
+    times = (_Timing * len(tracers))()
+    sc = scene.as_c()
+    _check(library().rt_render_multi(ctxs, len(tracers), ctypes.byref(sc), _ptr(d), _ptr(org),
+                                     width, height, rb, re, _FORMATS[fmt], _ptr(out), times),
+           "rt_render_multi")
+    names = {RT_PATH_BINNED: "binned", RT_PATH_GENERIC: "generic"}
+    return out, [Timing(t.total_us, t.upload_us, t.kernel_us, t.download_us,
+                        names.get(t.path, "idle")) for t in times]
 
 
 class RayTracer:

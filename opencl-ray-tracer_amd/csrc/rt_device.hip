@@ -33,6 +33,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "rt_hip.h"
@@ -1747,6 +1748,42 @@ int rt_render(rt_ctx* ctx, const rt_scene* scene, const float ray_dir[4], const 
               int32_t out_format, void* host_out, rt_timing* timing) {
     return rt_render_path(ctx, scene, ray_dir, ray_origins, width, height, row_begin, row_end,
                           out_format, RT_PATH_AUTO, host_out, timing);
+}
+
+int rt_render_multi(rt_ctx* const* ctxs, int32_t num_ctx, const rt_scene* scene,
+                    const float ray_dir[4], const float* ray_origins, int32_t width,
+                    int32_t height, int32_t row_begin, int32_t row_end, int32_t out_format,
+                    void* host_out, rt_timing* timings) {
+    if (!ctxs || num_ctx <= 0 || !ray_dir || !host_out) return RT_ERR_INVALID_ARG;
+    for (int32_t i = 0; i < num_ctx; ++i)
+        if (!ctxs[i]) return RT_ERR_INVALID_ARG;
+    int rc = check_args(scene, width, height, row_begin, row_end, out_format);
+    if (rc) return rc;
+    // contiguous bands of whole rows, sizes differing by at most one; more
+    // contexts than rows leave the surplus ones idle
+    const int32_t rows = row_end - row_begin;
+    const int32_t n = std::min(num_ctx, rows);
+    const size_t row_bytes = (size_t)width * (out_format == RT_FORMAT_I32X4 ? 16 : 4);
+    std::vector<int> status((size_t)n, RT_OK);
+    auto band = [&](int32_t i) {
+        const int32_t rb = row_begin + (int32_t)((int64_t)rows * i / n);
+        const int32_t re = row_begin + (int32_t)((int64_t)rows * (i + 1) / n);
+        char* dst = static_cast<char*>(host_out) + (size_t)(rb - row_begin) * row_bytes;
+        status[(size_t)i] = rt_render(ctxs[i], scene, ray_dir, ray_origins, width, height, rb,
+                                      re, out_format, dst, timings ? &timings[i] : nullptr);
+    };
+    if (n == 1) {
+        band(0);
+    } else {
+        std::vector<std::thread> workers;
+        workers.reserve((size_t)n);
+        for (int32_t i = 0; i < n; ++i) workers.emplace_back(band, i);
+        for (auto& w : workers) w.join();
+    }
+    for (int32_t i = n; timings && i < num_ctx; ++i) timings[i] = rt_timing{};
+    for (int s : status)
+        if (s != RT_OK) return s;
+    return RT_OK;
 }
 
 int rt_render_device(rt_ctx* ctx, const rt_scene* device_scene, const float ray_dir[4],

@@ -17,16 +17,15 @@
 // scene build and no scene upload.  The printed hash must equal the host
 // build's.
 //
-// --bands splits [A, B) into B row bands traced concurrently, one host
-// thread and one rt_ctx per band on device (band % D), each writing its rows
-// straight into the shared frame -- the reference's one pixels vector
+// --bands splits [A, B) into B row bands traced concurrently through
+// rt_render_multi, one rt_ctx per band on device (band % D), each writing its
+// rows straight into the shared frame -- the reference's one pixels vector
 // (MainState.cpp:676) assembled by disjoint row ranges, SURVEY.md §8(e).
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
-#include <thread>
 #include <vector>
 
 #include <hip/hip_runtime_api.h>
@@ -63,7 +62,6 @@ struct Band {
     int device = 0, row_begin = 0, row_end = 0;
     rt_ctx* ctx = nullptr;
     rt_timing timing{};
-    int status = RT_OK;
 };
 
 // --device-scene: the scene built and rendered on the device, frame read back.
@@ -200,30 +198,24 @@ int main(int argc, char** argv) {
     std::vector<int32_t> pixels(4 * (size_t)width * rows);
     if (device_scene) return render_device_scene(bands[0], width, height, row_begin, row_end,
                                                  syn_n, syn_m, seed, syn_k, ray_dir, pixels);
-    auto trace_band = [&](Band& band) {
-        int32_t* dst = pixels.data() + 4 * (size_t)width * (band.row_begin - row_begin);
-        band.status = rt_render(band.ctx, &scene, ray_dir, nullptr, width, height,
-                                band.row_begin, band.row_end, RT_FORMAT_I32X4, dst,
-                                &band.timing);
-    };
+    // rt_render_multi: one host thread and one context per band, each band's
+    // rows written straight into `pixels` (same row split as `bands`)
+    std::vector<rt_ctx*> ctxs;
+    for (Band& band : bands) ctxs.push_back(band.ctx);
+    std::vector<rt_timing> timings((size_t)n_bands);
     int status = 0;
     for (int r = 0; r < repeat && status == 0; ++r) {
         std::printf("HIP Ray Tracer Begin\n");
-        if (n_bands == 1) {
-            trace_band(bands[0]);
-        } else {
-            std::vector<std::thread> workers;
-            for (Band& band : bands) workers.emplace_back(trace_band, std::ref(band));
-            for (std::thread& w : workers) w.join();
+        rc = rt_render_multi(ctxs.data(), n_bands, &scene, ray_dir, nullptr, width, height,
+                             row_begin, row_end, RT_FORMAT_I32X4, pixels.data(), timings.data());
+        if (rc != RT_OK) {
+            std::fprintf(stderr, "rt_render_multi failed: %s\n", rt_error_string(rc));
+            status = 1;
+            break;
         }
         for (int b = 0; b < n_bands; ++b) {
-            const Band& band = bands[b];
-            if (band.status != RT_OK) {
-                std::fprintf(stderr, "rt_render failed (band %d): %s\n", b,
-                             rt_error_string(band.status));
-                status = 1;
-                continue;
-            }
+            Band& band = bands[b];
+            band.timing = timings[(size_t)b];
             const rt_timing& t = band.timing;
             std::printf("Time Taken: %.0f microseconds (upload %.1f, kernels %.1f, readback %.1f; "
                         "%s path)",

@@ -57,6 +57,14 @@ def test_argument_validation_without_gpu(pkg):
     assert lib.rt_render_device(None, ctypes.byref(c), d.ctypes.data, None, 2, 2, 0, 2, 0, 0,
                                 out.ctypes.data, None) == pkg.RT_ERR_INVALID_ARG
     assert lib.rt_init(0, None) == pkg.RT_ERR_INVALID_ARG
+    # rt_render_multi: no contexts / a NULL context
+    ctxs = (ctypes.c_void_p * 2)(None, None)
+    assert lib.rt_render_multi(None, 1, ctypes.byref(c), d.ctypes.data, None, 2, 2, 0, 2, 0,
+                               out.ctypes.data, None) == pkg.RT_ERR_INVALID_ARG
+    assert lib.rt_render_multi(ctxs, 0, ctypes.byref(c), d.ctypes.data, None, 2, 2, 0, 2, 0,
+                               out.ctypes.data, None) == pkg.RT_ERR_INVALID_ARG
+    assert lib.rt_render_multi(ctxs, 2, ctypes.byref(c), d.ctypes.data, None, 2, 2, 0, 2, 0,
+                               out.ctypes.data, None) == pkg.RT_ERR_INVALID_ARG
 
 
 def test_init_without_gpu_reports_no_device(pkg):

@@ -629,3 +629,29 @@ def test_profile_slots_of_skipped_kernels(pkg, rt):
                 assert (prof[key] > 0) == on, (path, key, prof)
     finally:
         rt.profile(False)
+
+
+@pytest.mark.parametrize("n_ctx", [1, 2, 3, 5])
+def test_render_multi_bands(pkg, rt, oracle, n_ctx):
+    """rt_render_multi: the frame split over n contexts (all on the one GPU
+    here, one host thread each) equals the single-context frame, for whole
+    frames, odd row ranges, both formats and more contexts than rows."""
+    scene = pkg.Scene.synthetic(700, 301, 300, 40, seed=n_ctx, k=1.5)
+    tracers = [rt] + [pkg.RayTracer(0) for _ in range(n_ctx - 1)]
+    try:
+        full, _ = rt.render(scene, 700, 301)
+        got, times = pkg.render_multi(tracers, scene, 700, 301)
+        assert np.array_equal(got, full)
+        assert len(times) == n_ctx and all(t.path == "binned" for t in times)
+        got, _ = pkg.render_multi(tracers, scene, 700, 301, rows=(33, 290))
+        assert np.array_equal(got, full[33:290])
+        tex, _ = pkg.render_multi(tracers, scene, 700, 301, fmt="rgba8")
+        assert np.array_equal(tex, pkg.pack_rgba8(full))
+        got, times = pkg.render_multi(tracers, scene, 700, 301, rows=(100, 102))
+        assert np.array_equal(got, full[100:102])
+        assert sum(t.path == "idle" for t in times) == max(0, n_ctx - 2)
+    finally:
+        for t in tracers[1:]:
+            t.close()
+    want = oracle.trace(scene, 700, 301, threads=THREADS)
+    assert not diff_report(full, want), diff_report(full, want)
