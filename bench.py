@@ -267,12 +267,21 @@ def main():
         c0 = time.perf_counter()
         orc.trace_rows(scene, w, full_h, sample_rows, threads=threads)
         c_s = time.perf_counter() - c0
+        # SURVEY.md §8d CPU baseline (a): the serial path on one core, on a
+        # deterministic row subset (every 32nd row of the same frame)
+        serial_rows = list(range(rb, re, 32))
+        c1 = time.perf_counter()
+        orc.trace_rows(scene, w, full_h, serial_rows, threads=1)
+        s_s = time.perf_counter() - c1
         cpu = {"value": len(sample_rows) * w / c_s / 1e6, "unit": "Mrays/s", "cores": threads,
                "kind": "port",
                "sample": (f"the whole {w}x{len(sample_rows)} frame" if args.cpu_rows == 1 else
                           f"{len(sample_rows)} rows (every {args.cpu_rows}th of rank 0's band) x {w}"
                           f" px") + f" of the same scene, oracle/rt_oracle.c orc_trace_rows_mt on "
-                         f"{threads} threads, {c_s:.1f} s wall"}
+                         f"{threads} threads, {c_s:.1f} s wall",
+               "serial_1core": {"value": round(len(serial_rows) * w / s_s / 1e6, 3),
+                                "sample": f"every 32nd row ({len(serial_rows)} rows x {w} px), "
+                                          f"1 thread, {s_s:.1f} s wall"}}
 
     # BASELINE.json config names, by the per-rank workload
     names = {(1920, 1080, 16, 4): "config2", (4096, 4096, 256, 64): "config3",
