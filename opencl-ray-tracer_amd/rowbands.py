@@ -85,11 +85,63 @@ def gather_frame(band: "torch.Tensor", height: int, world: int, rank: int, root:
     return torch.cat(parts)
 
 
+def interleaved_blocks(height: int, world: int, rank: int, block: int = 64) -> List[Tuple[int, int]]:
+    """Row blocks of `block` rows dealt round-robin over the ranks (SURVEY.md
+    §8e: for scenes whose load is not uniform down the frame).  64 rows is
+    one coarse bin row, so no bin is split between ranks."""
+    if not (0 <= rank < world) or height <= 0 or block <= 0:
+        raise ValueError("bad block request")
+    starts = range(rank * block, height, world * block)
+    return [(s, min(s + block, height)) for s in starts]
+
+
+def gather_frame_interleaved(blocks: "torch.Tensor", height: int, world: int, rank: int,
+                             block: int = 64, root: int = 0,
+                             group=None) -> Optional["torch.Tensor"]:
+    """Assemble the frame on `root` from every rank's interleaved row blocks
+    (this rank's blocks concatenated in order): one padded gather, then the
+    root puts every rank's blocks back in frame order."""
+    import torch
+    import torch.distributed as dist
+
+    counts = [sum(e - s for s, e in interleaved_blocks(height, world, r, block))
+              for r in range(world)]
+    max_rows = max(counts)
+    rows = blocks.shape[0]
+    if rows < max_rows:
+        pad = torch.zeros((max_rows - rows,) + tuple(blocks.shape[1:]), dtype=blocks.dtype,
+                          device=blocks.device)
+        send = torch.cat([blocks, pad])
+    else:
+        send = blocks.contiguous()
+    gl: Optional[List[torch.Tensor]] = (
+        [torch.empty_like(send) for _ in range(world)] if rank == root else None)
+    dist.gather(send, gl, dst=root, group=group)
+    if rank != root:
+        return None
+    frame = torch.empty((height,) + tuple(send.shape[1:]), dtype=send.dtype, device=send.device)
+    for r in range(world):
+        at = 0
+        for s, e in interleaved_blocks(height, world, r, block):
+            frame[s:e] = gl[r][at:at + (e - s)]
+            at += e - s
+    return frame
+
+
 def render_distributed(render_band: Callable[[int, int], "torch.Tensor"], height: int,
-                       world: int, rank: int, root: int = 0,
-                       group=None) -> Optional["torch.Tensor"]:
-    """render_band(row_begin, row_end) -> this rank's band tensor; the frame
-    is returned on root, None elsewhere."""
+                       world: int, rank: int, root: int = 0, group=None,
+                       interleave: int = 0) -> Optional["torch.Tensor"]:
+    """render_band(row_begin, row_end) -> that band's tensor; the frame is
+    returned on root, None elsewhere.  interleave > 0 deals row blocks of
+    that many rows round-robin instead of one contiguous band per rank."""
+    if interleave > 0:
+        import torch
+
+        parts = [render_band(s, e) for s, e in interleaved_blocks(height, world, rank, interleave)]
+        # a rank with no block still sends a (padded) empty part
+        blocks = torch.cat(parts) if parts else render_band(0, 1)[:0]
+        return gather_frame_interleaved(blocks, height, world, rank, interleave, root=root,
+                                        group=group)
     rb, re = band_rows(height, world, rank)
     band = render_band(rb, re)
     return gather_frame(band, height, world, rank, root=root, group=group)

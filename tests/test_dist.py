@@ -21,7 +21,7 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, width, height, scene_id, result_path):
+def _worker(rank, world, port, width, height, scene_id, result_path, interleave=0):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     sys.path.insert(0, str(REPO))
     sys.path.insert(0, str(REPO / "tests"))
@@ -47,20 +47,22 @@ def _worker(rank, world, port, width, height, scene_id, result_path):
         def render_band(rb, re):
             return torch.from_numpy(oracle.trace(ns, width, height, rows=(rb, re)))
 
-        frame = rowbands.render_distributed(render_band, height, world, rank)
+        frame = rowbands.render_distributed(render_band, height, world, rank,
+                                            interleave=interleave)
         if rank == 0:
             np.save(result_path, frame.numpy())
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("height,scene_id", [(480, 1), (97, 3)])
-def test_two_rank_row_bands_gloo(tmp_path, oracle, height, scene_id):
+@pytest.mark.parametrize("height,scene_id,interleave", [(480, 1, 0), (97, 3, 0), (480, 1, 64),
+                                                       (200, 3, 64), (97, 2, 16)])
+def test_two_rank_row_bands_gloo(tmp_path, oracle, height, scene_id, interleave):
     import torch.multiprocessing as mp
 
     width, world = 640, 2
     out = tmp_path / "frame.npy"
-    mp.spawn(_worker, args=(world, _free_port(), width, height, scene_id, str(out)),
+    mp.spawn(_worker, args=(world, _free_port(), width, height, scene_id, str(out), interleave),
              nprocs=world, join=True)
     frame = np.load(out)
     want = oracle.trace(oracle.scene_reference(scene_id, 1), width, height)
@@ -82,3 +84,18 @@ def test_band_rows_partition():
             assert all(a[1] == b[0] for a, b in zip(bands, bands[1:]))
             sizes = [e - b for b, e in bands]
             assert max(sizes) - min(sizes) <= 1
+
+
+def test_interleaved_blocks_partition():
+    sys.path.insert(0, str(REPO))
+    import __graft_entry__
+    __graft_entry__.load_package()
+    from opencl_ray_tracer_amd.rowbands import interleaved_blocks
+
+    for h in (1, 63, 64, 65, 480, 4097):
+        for world in (1, 2, 3, 8):
+            rows = sorted(r for rank in range(world)
+                          for s, e in interleaved_blocks(h, world, rank) for r in range(s, e))
+            assert rows == list(range(h))
+            for rank in range(world):
+                assert all(s % 64 == 0 for s, _ in interleaved_blocks(h, world, rank))
