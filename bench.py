@@ -57,6 +57,9 @@ def parse():
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--no-host-path", action="store_true",
                     help="skip the end-to-end rt_render (host buffers) measurement")
+    ap.add_argument("--path", choices=("auto", "binned", "generic"), default="auto",
+                    help="kernel path: generic = the brute-force per-pixel kernel (every ray "
+                         "against every primitive), for the compute-bound comparison")
     ap.add_argument("--trace-mode", type=int, default=0,
                     help="diagnostics ablation: 1 = stores only, 2 = no per-pixel tests")
     ap.add_argument("--pmc", default=str(REPO / "profiles" / "r01_pmc_config3.json"),
@@ -120,7 +123,7 @@ def main():
 
     # ctypes arguments built once; each step enqueues prep + coarse + trace
     step = rt.bind_render_device(dscene, w, full_h, (rb, re), out.data_ptr(), fmt=args.format,
-                                 stream=stream.cuda_stream)
+                                 path=args.path, stream=stream.cuda_stream)
 
     def barrier():
         if distributed:
@@ -186,7 +189,8 @@ def main():
 
     traffic = None
     pmc_path = Path(args.pmc)
-    if world == 1 and pmc_path.exists():  # measured for the 1-GPU workload only
+    # measured for the 1-GPU workload of the real binned trace kernel only
+    if world == 1 and args.path != "generic" and args.trace_mode == 0 and pmc_path.exists():
         try:
             pmc = json.loads(pmc_path.read_text())
             if pmc.get("config") == [w, rows, args.spheres, args.cubes, args.seed, args.format]:
@@ -289,6 +293,8 @@ def main():
     workload = names.get((w, rows, args.spheres, args.cubes), "custom")
     # the dominant kernel: scenes of at most 512 primitives take trace_small_kernel
     kernel = "trace_small_kernel" if 0 < n_sph + 12 * n_cub <= 512 else "trace3_kernel"
+    if args.path == "generic":
+        kernel = "generic_kernel"
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "Mrays/s", "n_gpus": world,
