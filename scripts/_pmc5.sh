@@ -1,0 +1,11 @@
+set -u
+R=$GRAFT_REPO_ROOT; cd /tmp; export TMPDIR=/tmp
+ARGS="--steps 3 --warmup 1 --no-cpu-baseline --no-host-path --width 16384 --height 16384 --spheres 4096 --cubes 0"
+i=0
+for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM GRBM_GUI_ACTIVE" \
+           "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU"; do
+  i=$((i+1))
+  timeout -k 10 200 rocprofv3 --kernel-trace --pmc $grp -d "$R/gpurun_out/pmc5_$i" -o run --output-format csv -- python "$R/bench.py" $ARGS > "$R/gpurun_out/pmc5_$i.log" 2>&1
+  rc=$?; echo "pass $i rc=$rc"; [ $rc -ne 0 ] && exit $rc
+done
+exit 0
