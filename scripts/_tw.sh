@@ -1,7 +1,7 @@
 set -u
 cd $GRAFT_REPO_ROOT
 V=opencl-ray-tracer_amd/variants
-L="$V/librt_hip_base.so $V/librt_hip_o1000.so $V/librt_hip_o950.so $V/librt_hip_o900.so"
+L="$V/librt_hip_base.so $V/librt_hip_p1.so $V/librt_hip_p3.so"
 echo "== config 3"
 timeout -k 10 300 python scripts/bench_variants.py $L --rounds 11 2>&1 | grep -v amdgpu.ids || exit 3
 echo "== config 5 dense"
