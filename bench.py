@@ -3,17 +3,31 @@
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
 
-A step = one full pass of the hot path over one frame band: the prep, bin
-and trace kernels of librt_hip.so on a scene already resident in HBM,
-writing the int32x4 framebuffer band to HBM (rt_render_device).
+Workload (BASELINE config 3, the headline): one 4096x4096 frame, 256
+spheres + 64 cubes, dense synthetic scene (seed 3, k =
+4096/640), int32x4 framebuffer (16 B/ray), scene resident in HBM.
 
-Workload at N=1 is BASELINE config 3: 4096x4096, 256 spheres + 64 cubes,
-dense synthetic scene (seed 3, k = 4096/640).  With N ranks
-the image grows to 4096 x (4096 N) with N x (256 + 64) primitives of the
-same density and rank r renders rows [4096 r, 4096 (r+1)): per-GPU work is
-fixed (weak scaling), no collective sits in the timed region.  The RCCL
-gather that assembles the frame on rank 0 (north_star's Texture assembly)
-is measured separately and reported under "gather".
+A step at N=1: one pass of the hot path over the frame -- the prep, bin and
+trace kernels of librt_hip.so writing the frame to HBM (rt_render_device).
+
+A step at N>1 (strong scaling): the SAME frame split into
+N contiguous row bands, one per rank, and the frame assembled on rank 0.  The
+clock runs from the barrier before the renders to the assembled frame on rank
+0 (max over ranks), so the transfer is inside `value`.  Two assemblies are
+measured and the faster is `value` (both are reported, each checked
+bit-exactly against a one-GPU render of the whole frame on rank 0):
+  rccl_p2p         every rank renders its band locally, then RCCL
+                   point-to-point sends land it in rank 0's frame rows
+                   (rank 0 renders its own band in place);
+  xgmi_peer_store  rank 0's frame is mapped into every rank (IPC handle,
+                   rt_shared_open) and each rank's trace kernel stores its
+                   band straight into it over xGMI; a one-element RCCL
+                   all-reduce after the render tells rank 0 all bands landed.
+Also reported at N>1: the render/assembly split, the RGBA8 Texture form of
+the same assembly (4 B/ray, the north_star's Texture), BASELINE config 4
+(8192^2, 192 + 64, seed 4) with the same assembly, and weak scaling (each
+rank renders a 4096x4096 band of a 4096 x 4096N frame, no assembly) as a
+secondary key -- never as `value`.
 
 Rank 0 prints ONE JSON line.
 """
@@ -35,28 +49,35 @@ import __graft_entry__  # noqa: E402
 METRIC = "Mrays/sec (primary) at 4096×4096, 1/2/4/8 MI355X; % HBM-write roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec); 6.29 TB/s measured copy
 BYTES_PER_RAY = {"i32x4": 16, "rgba8": 4}
+# BASELINE.json configs by (width, height, spheres, cubes)
+CONFIG_NAMES = {(1920, 1080, 16, 4): "config2", (4096, 4096, 256, 64): "config3",
+                (8192, 8192, 192, 64): "config4", (16384, 16384, 4096, 0): "config5"}
+CONFIG4 = dict(width=8192, height=8192, spheres=192, cubes=64, seed=4)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--width", type=int, default=4096)
-    ap.add_argument("--height", type=int, default=4096, help="rows per rank")
-    ap.add_argument("--spheres", type=int, default=256, help="per rank")
-    ap.add_argument("--cubes", type=int, default=64, help="per rank")
+    ap.add_argument("--height", type=int, default=4096, help="frame rows (all ranks together)")
+    ap.add_argument("--spheres", type=int, default=256)
+    ap.add_argument("--cubes", type=int, default=64)
     ap.add_argument("--seed", type=int, default=3)
     ap.add_argument("--k", type=float, default=None, help="object scale (default width/640)")
     ap.add_argument("--format", choices=sorted(BYTES_PER_RAY), default="i32x4")
     ap.add_argument("--cpu-rows", type=int, default=1,
-                    help="CPU baseline samples every Nth row of rank 0's band (1 = the "
-                         "whole band: the full config-3 frame at N=1, ~4 s on 16 threads)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+                    help="CPU baseline samples every Nth row of the frame (1 = the whole "
+                         "frame: ~4 s for config 3 on 16 threads)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline threads (0 = every CPU this job may use: the "
+                         "affinity set, capped by the job's CPU share OMP_NUM_THREADS)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--no-host-path", action="store_true",
                     help="skip the end-to-end rt_render (host buffers) measurement")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="N>1: time only the headline assemblies (no Texture / config 4 / weak)")
     ap.add_argument("--path", choices=("auto", "binned", "generic"), default="auto",
                     help="kernel path: generic = the brute-force per-pixel kernel (every ray "
                          "against every primitive), for the compute-bound comparison")
@@ -69,188 +90,194 @@ def parse():
     ap.add_argument("--rehearse", action="store_true",
                     help="N>1 rehearsal on a 1-GPU box: every rank renders on cuda:0 and the "
                          "collectives run over gloo on host copies")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
-def main():
-    args = parse()
-    import torch
-    import torch.distributed as dist
+# ---------------------------------------------------------------------------
+# arithmetic shared by the N=1 and N>1 lines (checked by tests/test_bench.py)
+# ---------------------------------------------------------------------------
+def mrays_per_s(rays: int, ms: float) -> float:
+    return rays / (ms * 1e-3) / 1e6
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and not (world == 1 and args.gpus == 1):
-        if world == 1:
+
+def bytes_to_root(width: int, height: int, world: int, fmt: str, root: int = 0) -> int:
+    """Framebuffer bytes that must reach the root: every band but its own."""
+    from opencl_ray_tracer_amd.rowbands import band_rows
+
+    rb, re = band_rows(height, world, root)
+    return BYTES_PER_RAY[fmt] * width * (height - (re - rb))
+
+
+def pick_value(assemblies: dict):
+    """The fastest assembly whose frame was bit-exact: (name, entry)."""
+    ok = [(v["ms_per_step"], k) for k, v in assemblies.items()
+          if v.get("ms_per_step") is not None and v.get("frame_check") == "bit-exact"]
+    if not ok:
+        raise RuntimeError(f"no assembly produced a bit-exact frame: {assemblies}")
+    ms, name = min(ok)
+    return name, assemblies[name]
+
+
+def cpu_threads(requested: int) -> tuple:
+    """(threads to use, description).  0 = every CPU this job may run on:
+    the affinity set, capped by the job's CPU share where the launcher
+    states one (OMP_NUM_THREADS; the GPU box grants 16 CPUs per GPU)."""
+    affinity = len(os.sched_getaffinity(0))
+    share = os.environ.get("OMP_NUM_THREADS")
+    n = affinity
+    if share and share.isdigit() and int(share) > 0:
+        n = min(n, int(share))
+    if requested > 0:
+        n = min(requested, affinity)
+    return max(1, n), {"affinity_cpus": affinity, "os_cpu_count": os.cpu_count(),
+                       "omp_num_threads": share}
+
+
+class Ctx:
+    """Process / device / collective plumbing of one bench run."""
+
+    def __init__(self, args):
+        import torch
+        import torch.distributed as dist
+
+        self.torch, self.dist = torch, dist
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        if self.world != args.gpus and self.world == 1 and args.gpus != 1:
             raise SystemExit(f"--gpus {args.gpus} needs torchrun with {args.gpus} ranks")
-    distributed = world > 1
-    backend = "gloo" if args.rehearse else args.backend
-    gpu = 0 if args.rehearse else local
-    if distributed:
-        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        torch.cuda.set_device(gpu)
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
-        else:
-            dist.init_process_group("gloo")
-    dev = torch.device("cuda", gpu)
-    # collectives run on the GPU tensors with RCCL, on host copies with gloo
-    coll_dev = dev if backend == "nccl" else torch.device("cpu")
+        self.distributed = self.world > 1
+        self.backend = "gloo" if args.rehearse else args.backend
+        self.gpu = 0 if args.rehearse else local
+        if self.distributed:
+            os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+            torch.cuda.set_device(self.gpu)
+            if self.backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", self.gpu))
+            else:
+                dist.init_process_group("gloo")
+        self.dev = torch.device("cuda", self.gpu)
+        # collectives move GPU tensors with RCCL, host copies with gloo
+        self.coll_dev = self.dev if self.backend == "nccl" else torch.device("cpu")
+        # A real stream object: the legacy default stream's handle is 0, which
+        # the C ABI reads as "the context's own stream".
+        self.stream = torch.cuda.Stream(self.dev)
+        torch.cuda.set_stream(self.stream)
 
-    pkg = __graft_entry__.load_package()
-    w, rows = args.width, args.height
-    full_h = rows * world
-    k = args.k if args.k is not None else w / 640.0
-    n_sph, n_cub = args.spheres * world, args.cubes * world
-    scene = pkg.Scene.synthetic(w, full_h, n_sph, n_cub, seed=args.seed, k=k)
-    rb, re = rank * rows, (rank + 1) * rows
+    def barrier(self):
+        if self.distributed:
+            self.dist.barrier()
 
-    rt = pkg.RayTracer(gpu)
-    rt.set_trace_mode(args.trace_mode)
-    t = {name: torch.from_numpy(np.ascontiguousarray(getattr(scene, name))).to(dev)
+    def sync(self):
+        self.torch.cuda.synchronize(self.dev)
+
+    def max_over_ranks(self, v: float) -> float:
+        if not self.distributed:
+            return v
+        t = self.torch.tensor([v], dtype=self.torch.float64, device=self.coll_dev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def timed(self, step, steps: int, events=None) -> float:
+        """`steps` calls of step() between barrier + sync; this rank's clock
+        stops at its own sync (the trailing barrier's latency is outside it);
+        returns the max over ranks of wall ms per step.  `events`: a pair of
+        torch.cuda.Event recorded on the stream around the K steps."""
+        self.sync()
+        self.barrier()
+        self.sync()
+        t0 = time.perf_counter()
+        if events:
+            events[0].record(self.stream)
+        for _ in range(steps):
+            step()
+        if events:
+            events[1].record(self.stream)
+        self.sync()
+        wall = (time.perf_counter() - t0) * 1e3 / steps
+        self.barrier()
+        return self.max_over_ranks(wall)
+
+
+def device_scene(pkg, c: Ctx, width, height, spheres, cubes, seed, k):
+    scene = pkg.Scene.synthetic(width, height, spheres, cubes, seed=seed, k=k)
+    t = {name: c.torch.from_numpy(np.ascontiguousarray(getattr(scene, name))).to(c.dev)
          for name in ("sphere_origins", "sphere_radius", "sphere_colours", "cube_vertices",
                       "cube_colours")}
-    dscene = {name: v.data_ptr() for name, v in t.items()}
-    dscene.update(num_spheres=scene.num_spheres, num_cubes=scene.num_cubes)
-    if args.format == "i32x4":
-        out = torch.empty((rows, w, 4), dtype=torch.int32, device=dev)
-    else:
-        out = torch.empty((rows, w), dtype=torch.int32, device=dev)
-    # A real stream object: the legacy default stream's handle is 0, which the
-    # C ABI reads as "the context's own stream".
-    stream = torch.cuda.Stream(dev)
-    torch.cuda.set_stream(stream)
+    ds = {name: v.data_ptr() for name, v in t.items()}
+    ds.update(num_spheres=scene.num_spheres, num_cubes=scene.num_cubes)
+    ds["_keep"] = t
+    return scene, ds
 
+
+def frame_tensor(c: Ctx, rows, width, fmt):
+    shape = (rows, width, 4) if fmt == "i32x4" else (rows, width)
+    return c.torch.empty(shape, dtype=c.torch.int32, device=c.dev)
+
+
+# ---------------------------------------------------------------------------
+# N = 1
+# ---------------------------------------------------------------------------
+def run_single(args, c: Ctx, pkg):
+    torch = c.torch
+    w, h = args.width, args.height
+    k = args.k if args.k is not None else w / 640.0
+    scene, ds = device_scene(pkg, c, w, h, args.spheres, args.cubes, args.seed, k)
+    rt = pkg.RayTracer(c.gpu)
+    rt.set_trace_mode(args.trace_mode)
+    out = frame_tensor(c, h, w, args.format)
     # ctypes arguments built once; each step enqueues prep + coarse + trace
-    step = rt.bind_render_device(dscene, w, full_h, (rb, re), out.data_ptr(), fmt=args.format,
-                                 path=args.path, stream=stream.cuda_stream)
-
-    def barrier():
-        if distributed:
-            dist.barrier()
-
+    step = rt.bind_render_device(ds, w, h, (0, h), out.data_ptr(), fmt=args.format,
+                                 path=args.path, stream=c.stream.cuda_stream)
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize(dev)
-    barrier()
-    torch.cuda.synchronize(dev)
-
-    def timed(profiled: bool):
-        """K steps between barrier + sync on both sides; wall ms per step
-        (max over ranks) and the stream-event ms per step."""
-        rt.profile(profiled)
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        torch.cuda.synchronize(dev)
-        barrier()
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        ev0.record(stream)
-        for _ in range(args.steps):
-            step()
-        ev1.record(stream)
-        torch.cuda.synchronize(dev)
-        # this rank's K steps end here; the trailing barrier's own latency
-        # (an RCCL all-reduce, tens of us) is not part of them.  The max over
-        # ranks below is the job's time: every rank started at the barrier.
-        wall = (time.perf_counter() - t0) * 1e3 / args.steps
-        barrier()
-        torch.cuda.synchronize(dev)
-        rt.profile(False)
-        if distributed:
-            tt = torch.tensor([wall], device=coll_dev)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            wall = float(tt.item())
-        return wall, ev0.elapsed_time(ev1) / args.steps
+    c.sync()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 
     # The timed region: K steps, nothing attached to the kernels.
-    wall_ms, event_ms = timed(False)
+    wall_ms = c.timed(step, args.steps, events=(ev0, ev1))
+    event_ms = ev0.elapsed_time(ev1) / args.steps
 
     # Per-kernel durations: the same K steps again with start/stop HIP events
     # attached to each kernel's own dispatch packet on the launch stream
     # (hipExtLaunchKernelGGL; events from a pool grown in an untimed pass).
     # Not the timed region itself: with the events attached the wall time per
-    # step grows by 25-40% (58-60 -> 73-85 us measured), while the kernels'
-    # own durations agree with rocprofv3's.
+    # step grows by 25-40%, while the kernels' own durations agree with
+    # rocprofv3's.
     rt.profile(True)
     for _ in range(args.steps):  # untimed: grows the event pool to K renders
         step()
-    torch.cuda.synchronize(dev)
+    c.sync()
     rt.profile_read()
-    prof_wall_ms, _ = timed(True)
+    rt.profile(True)
+    prof_wall_ms = c.timed(step, args.steps)
     prof = rt.profile_read()
+    rt.profile(False)
     n = max(prof["renders"], 1)
-    trace_ms = prof["trace_ms"] / n
-    prep_ms, bin_ms = prof["prep_ms"] / n, prof["bin_ms"] / n
+    trace_ms, prep_ms, bin_ms = prof["trace_ms"] / n, prof["prep_ms"] / n, prof["bin_ms"] / n
 
-    rays_rank = w * rows
-    value = world * rays_rank / (wall_ms * 1e-3) / 1e6
-    algo_bytes = BYTES_PER_RAY[args.format] * rays_rank
+    rays = w * h
+    algo_bytes = BYTES_PER_RAY[args.format] * rays
     achieved = algo_bytes / (trace_ms * 1e-3) / 1e9
-
     traffic = None
     pmc_path = Path(args.pmc)
-    # measured for the 1-GPU workload of the real binned trace kernel only
-    if world == 1 and args.path != "generic" and args.trace_mode == 0 and pmc_path.exists():
+    # measured for this workload of the real binned trace kernel only
+    if args.path != "generic" and args.trace_mode == 0 and pmc_path.exists():
         try:
             pmc = json.loads(pmc_path.read_text())
-            if pmc.get("config") == [w, rows, args.spheres, args.cubes, args.seed, args.format]:
+            if pmc.get("config") == [w, h, args.spheres, args.cubes, args.seed, args.format]:
                 traffic = pmc.get("hbm_bytes_per_launch")
         except (ValueError, OSError):
             traffic = None
 
-    gather = None
-    if distributed and not args.no_gather:
-        # Texture assembly on rank 0 (north_star): one RCCL gather of the bands.
-        from opencl_ray_tracer_amd import rowbands
-
-        band = out if coll_dev == dev else out.cpu()
-        for _ in range(2):
-            rowbands.gather_frame(band, full_h, world, rank)
-        torch.cuda.synchronize(dev)
-        barrier()
-        g0 = time.perf_counter()
-        reps = max(3, args.steps // 4)
-        for _ in range(reps):
-            rowbands.gather_frame(band, full_h, world, rank)
-        torch.cuda.synchronize(dev)
-        barrier()
-        g_ms = (time.perf_counter() - g0) * 1e3 / reps
-        gather = {"collective": f"{'rccl' if backend == 'nccl' else 'gloo (host)'} gather of "
-                                f"row bands to rank 0", "ms": round(g_ms, 4),
-                  "bytes_to_root": algo_bytes * (world - 1),
-                  "render_plus_gather_mrays": round(
-                      world * rays_rank / ((wall_ms + g_ms) * 1e-3) / 1e6, 1)}
-        if args.format == "i32x4":
-            # The Texture assembly (SURVEY.md §8e): the same bands rendered in
-            # the Texture's RGBA8 packing (MainState.cpp:1023-1037) gather 4x
-            # fewer bytes.  Rendered once, untimed; the gather is timed alone.
-            tex = torch.empty((rows, w), dtype=torch.int32, device=dev)
-            rt.bind_render_device(dscene, w, full_h, (rb, re), tex.data_ptr(), fmt="rgba8",
-                                  stream=stream.cuda_stream)()
-            torch.cuda.synchronize(dev)
-            tband = tex if coll_dev == dev else tex.cpu()
-            for _ in range(2):
-                rowbands.gather_frame(tband, full_h, world, rank)
-            torch.cuda.synchronize(dev)
-            barrier()
-            g0 = time.perf_counter()
-            for _ in range(reps):
-                rowbands.gather_frame(tband, full_h, world, rank)
-            torch.cuda.synchronize(dev)
-            barrier()
-            t_ms = (time.perf_counter() - g0) * 1e3 / reps
-            gather["texture_rgba8"] = {"ms": round(t_ms, 4),
-                                       "bytes_to_root": 4 * rays_rank * (world - 1)}
-
     host = None
-    if world == 1 and not args.no_host_path:
+    if not args.no_host_path:
         # SURVEY.md §8f row f4: the reference's timer scope (MainState.cpp:
         # 662-894: scene upload, render, blocking readback of the frame),
         # through the synchronous host-buffer entry point rt_render.  Never
         # `value`: it includes the PCIe copy of the whole frame.
         host_buf = np.empty(tuple(out.shape), np.int32 if args.format == "i32x4" else np.uint32)
-        runs = [rt.render(scene, w, full_h, fmt=args.format, out=host_buf)[1]
-                for _ in range(4)][1:]
+        runs = [rt.render(scene, w, h, fmt=args.format, out=host_buf)[1] for _ in range(4)][1:]
         best = min(runs, key=lambda t: t.total_us)
         host = {"scope": "rt_render: scene upload + kernels + frame download (PCIe) into a "
                          "reused host buffer",
@@ -258,71 +285,308 @@ def main():
                 "upload_ms": round(best.upload_us / 1e3, 3),
                 "kernel_ms": round(best.kernel_us / 1e3, 3),
                 "download_ms": round(best.download_us / 1e3, 3),
-                "mrays_end_to_end": round(rays_rank / best.total_us, 1)}
+                "mrays_end_to_end": round(rays / best.total_us, 1)}
 
-    cpu = None
-    if world == 1 and not args.no_cpu_baseline:  # rank 0 at N=1 only
-        sys.path.insert(0, str(REPO / "tests"))
-        from oracle_lib import Oracle  # CPU baseline only
-
-        threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-        orc = Oracle()
-        sample_rows = list(range(rb, re, args.cpu_rows))
-        c0 = time.perf_counter()
-        orc.trace_rows(scene, w, full_h, sample_rows, threads=threads)
-        c_s = time.perf_counter() - c0
-        # SURVEY.md §8d CPU baseline (a): the serial path on one core, on a
-        # deterministic row subset (every 32nd row of the same frame)
-        serial_rows = list(range(rb, re, 32))
-        c1 = time.perf_counter()
-        orc.trace_rows(scene, w, full_h, serial_rows, threads=1)
-        s_s = time.perf_counter() - c1
-        cpu = {"value": len(sample_rows) * w / c_s / 1e6, "unit": "Mrays/s", "cores": threads,
-               "kind": "port",
-               "sample": (f"the whole {w}x{len(sample_rows)} frame" if args.cpu_rows == 1 else
-                          f"{len(sample_rows)} rows (every {args.cpu_rows}th of rank 0's band) x {w}"
-                          f" px") + f" of the same scene, oracle/rt_oracle.c orc_trace_rows_mt on "
-                         f"{threads} threads, {c_s:.1f} s wall",
-               "serial_1core": {"value": round(len(serial_rows) * w / s_s / 1e6, 3),
-                                "sample": f"every 32nd row ({len(serial_rows)} rows x {w} px), "
-                                          f"1 thread, {s_s:.1f} s wall"}}
-
-    # BASELINE.json config names, by the per-rank workload
-    names = {(1920, 1080, 16, 4): "config2", (4096, 4096, 256, 64): "config3",
-             (8192, 8192, 192, 64): "config4", (16384, 16384, 4096, 0): "config5"}
-    workload = names.get((w, rows, args.spheres, args.cubes), "custom")
+    cpu = None if args.no_cpu_baseline else cpu_baseline(args, scene, w, h)
+    workload = CONFIG_NAMES.get((w, h, args.spheres, args.cubes), "custom")
     # the dominant kernel: scenes of at most 512 primitives take trace_small_kernel
-    kernel = "trace_small_kernel" if 0 < n_sph + 12 * n_cub <= 512 else "trace3_kernel"
-    if args.path == "generic":
-        kernel = "generic_kernel"
-    if rank == 0:
-        line = {
-            "metric": METRIC, "value": round(value, 1), "unit": "Mrays/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(wall_ms, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic",
-            "config": {"workload": f"{workload}: {w}x{rows} rows/rank, {args.spheres} spheres + "
-                                   f"{args.cubes} cubes per rank, dense k={k:.2f}, seed {args.seed}",
-                       "width": w, "rows_per_rank": rows, "image_height": full_h,
-                       "spheres": n_sph, "cubes": n_cub, "format": args.format,
-                       "parallelism": f"row-bands x{world}"
-                                      + (" (rehearsal: shared cuda:0, gloo)" if args.rehearse
-                                         else "")},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic, "kernel": kernel,
-                         "kernel_ms": round(trace_ms, 4), "prep_ms": round(prep_ms, 4),
-                         "bin_ms": round(bin_ms, 4), "algo_bytes_per_launch": algo_bytes},
-            "event_ms_per_step": round(event_ms, 4),
-            "profiled_pass_ms_per_step": round(prof_wall_ms, 4),
-            "cpu_baseline": cpu,
-            "gather": gather,
-            "host_path": host,
-        }
-        print(json.dumps(line), flush=True)
+    kernel = ("generic_kernel" if args.path == "generic" else
+              "trace_small_kernel" if 0 < args.spheres + 12 * args.cubes <= 512 else
+              "trace3_kernel")
     rt.close()
-    if distributed:
-        dist.destroy_process_group()
+    return {
+        "metric": METRIC, "value": round(mrays_per_s(rays, wall_ms), 1), "unit": "Mrays/s",
+        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(wall_ms, 4),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic",
+        "config": {"workload": f"{workload}: {w}x{h} frame, {args.spheres} spheres + "
+                               f"{args.cubes} cubes, dense k={k:.2f}, seed {args.seed}",
+                   "width": w, "height": h, "spheres": args.spheres, "cubes": args.cubes,
+                   "format": args.format, "parallelism": "1 GPU (the whole frame)"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": traffic, "kernel": kernel, "kernel_ms": round(trace_ms, 4),
+                     "prep_ms": round(prep_ms, 4), "bin_ms": round(bin_ms, 4),
+                     "algo_bytes_per_launch": algo_bytes},
+        "event_ms_per_step": round(event_ms, 4),
+        "profiled_pass_ms_per_step": round(prof_wall_ms, 4),
+        "cpu_baseline": cpu,
+        "host_path": host,
+    }
+
+
+def cpu_baseline(args, scene, w, h):
+    """The oracle (the serial CPU path restated, oracle/rt_oracle.c) timed on
+    this box's host CPUs: all CPUs the job may use, plus one core."""
+    sys.path.insert(0, str(REPO / "tests"))
+    from oracle_lib import Oracle  # CPU baseline only
+
+    threads, cpus = cpu_threads(args.cpu_threads)
+    orc = Oracle()
+    sample_rows = list(range(0, h, args.cpu_rows))
+    c0 = time.perf_counter()
+    orc.trace_rows(scene, w, h, sample_rows, threads=threads)
+    c_s = time.perf_counter() - c0
+    # SURVEY.md §8d CPU baseline (a): the serial path on one core, on a
+    # deterministic row subset (every 32nd row of the same frame)
+    serial_rows = list(range(0, h, 32))
+    c1 = time.perf_counter()
+    orc.trace_rows(scene, w, h, serial_rows, threads=1)
+    s_s = time.perf_counter() - c1
+    return {"value": round(len(sample_rows) * w / c_s / 1e6, 3), "unit": "Mrays/s",
+            "cores": threads, "kind": "port",
+            "host_cpus": cpus,
+            "sample": (f"the whole {w}x{len(sample_rows)} frame" if args.cpu_rows == 1 else
+                       f"{len(sample_rows)} rows (every {args.cpu_rows}th) x {w} px")
+                      + f" of the same scene, oracle/rt_oracle.c orc_trace_rows_mt on "
+                        f"{threads} threads (one row band per thread), {c_s:.1f} s wall",
+            "serial_1core": {"value": round(len(serial_rows) * w / s_s / 1e6, 3),
+                             "sample": f"every 32nd row ({len(serial_rows)} rows x {w} px), "
+                                       f"1 thread, {s_s:.1f} s wall"}}
+
+
+# ---------------------------------------------------------------------------
+# N > 1: strong scaling of one frame, assembled on rank 0
+# ---------------------------------------------------------------------------
+class Assembly:
+    """One frame (width x height, `fmt`) split into row bands over the ranks
+    and assembled on rank 0 by `how` ("rccl_p2p" or "xgmi_peer_store")."""
+
+    def __init__(self, c: Ctx, pkg, rt, ds, width, height, fmt, how, path="auto"):
+        from opencl_ray_tracer_amd import rowbands
+
+        self.c, self.rt, self.how, self.fmt = c, rt, how, fmt
+        self.width, self.height = width, height
+        self.rowbands = rowbands
+        self.rb, self.re = rowbands.band_rows(height, c.world, c.rank)
+        self.root = c.rank == 0
+        px_bytes = BYTES_PER_RAY[fmt]
+        self.row_bytes = width * px_bytes
+        self.error = None
+        self.shared = None
+        torch = c.torch
+        stream = c.stream.cuda_stream
+        empty = self.re <= self.rb
+        if how == "rccl_p2p":
+            self.frame = frame_tensor(c, height, width, fmt) if self.root else None
+            self.band = (self.frame[self.rb:self.re] if self.root
+                         else frame_tensor(c, self.re - self.rb, width, fmt))
+            if c.backend != "nccl":  # rehearsal: gloo moves host copies
+                self.host_frame = (torch.empty(self.frame.shape, dtype=torch.int32)
+                                   if self.root else None)
+            dst = self.band.data_ptr()
+        else:
+            self.shared = rowbands.SharedFrame(rt, self.row_bytes * height, self.row_bytes,
+                                               c.rank, handle_device=c.coll_dev)
+            if not self.shared.ok:
+                self.error = self.shared.error
+                return
+            self.signal = torch.zeros(1, dtype=torch.int32, device=c.coll_dev)
+            self.frame = None
+            if self.root:  # a torch view of the shared frame, for the check
+                self.frame = _wrap_device(c, self.shared.ptr, height, width, fmt)
+            dst = self.shared.ptr_of_row(self.rb)
+        self.render = (None if empty else
+                       rt.bind_render_device(ds, width, height, (self.rb, self.re), dst, fmt=fmt,
+                                             path=path, stream=stream))
+
+    def render_only(self):
+        if self.render:
+            self.render()
+
+    def assemble_only(self):
+        c = self.c
+        if self.how == "rccl_p2p":
+            if c.backend == "nccl":
+                for q in self.rowbands.assemble_frame(self.frame, self.band, self.height, c.world,
+                                                      c.rank, async_op=True):
+                    q.wait()  # the stream waits; the host does not
+            else:
+                c.sync()
+                hf = self.host_frame
+                self.rowbands.assemble_frame(hf, self.band.cpu(), self.height, c.world, c.rank)
+                if self.root:  # the other ranks' rows, host -> device
+                    for r in range(1, c.world):
+                        rb, re = self.rowbands.band_rows(self.height, c.world, r)
+                        self.frame[rb:re].copy_(hf[rb:re])
+        else:
+            # every band landed in rank 0's frame once every rank's render
+            # finished: a one-element all-reduce behind the render on each
+            # rank's stream (RCCL), or a host barrier after a sync (gloo)
+            if c.backend == "nccl":
+                c.dist.all_reduce(self.signal, async_op=True).wait()
+            else:
+                c.sync()
+                c.dist.barrier()
+
+    def step(self):
+        self.render_only()
+        self.assemble_only()
+
+    def check(self, ds) -> str:
+        """Rank 0: the assembled frame against a one-GPU render of the whole
+        frame (bit-exact or not); broadcast so every rank agrees."""
+        c = self.c
+        ok = c.torch.ones(1, dtype=c.torch.int32, device=c.coll_dev)
+        if self.root:
+            c.sync()
+            ref = frame_tensor(c, self.height, self.width, self.fmt)
+            self.rt.bind_render_device(ds, self.width, self.height, (0, self.height),
+                                       ref.data_ptr(), fmt=self.fmt,
+                                       stream=c.stream.cuda_stream)()
+            c.sync()
+            ok.fill_(int(c.torch.equal(ref, self.frame)))
+            del ref
+        c.dist.broadcast(ok, 0)
+        return "bit-exact" if int(ok.item()) else "MISMATCH"
+
+    def close(self):
+        if self.shared is not None:
+            self.c.sync()
+            self.shared.close()
+
+
+def _wrap_device(c: Ctx, ptr: int, rows, width, fmt):
+    """A torch int32 tensor viewing `rows` x `width` pixels at device address
+    `ptr` (memory owned by librt_hip.so, e.g. the shared frame)."""
+    torch = c.torch
+    shape = (rows, width, 4) if fmt == "i32x4" else (rows, width)
+
+    class _Arr:
+        __cuda_array_interface__ = {"shape": shape, "typestr": "<i4", "data": (ptr, False),
+                                    "version": 2, "strides": None}
+    return torch.as_tensor(_Arr(), device=c.dev)
+
+
+def measure_assembly(args, c, pkg, rt, ds, width, height, fmt, how, split=False):
+    a = Assembly(c, pkg, rt, ds, width, height, fmt, how)
+    if a.error:
+        a.close()  # frees what the root allocated; a barrier on every rank
+        return {"ms_per_step": None, "error": a.error}
+    for _ in range(args.warmup):
+        a.step()
+    c.sync()
+    ms = c.timed(a.step, args.steps)
+    res = {"ms_per_step": round(ms, 4),
+           "mrays": round(mrays_per_s(width * height, ms), 1),
+           "bytes_to_root": bytes_to_root(width, height, c.world, fmt)}
+    if split:
+        render_ms = c.timed(a.render_only, args.steps)
+        # rccl_p2p: the local render; xgmi_peer_store: the render whose
+        # stores go over xGMI into rank 0's frame, without the signal
+        res["render_ms"] = round(render_ms, 4)
+        if how == "rccl_p2p":
+            # the assembly alone (bands already rendered): its link rate
+            asm_ms = c.timed(a.assemble_only, args.steps)
+            res["assemble_ms"] = round(asm_ms, 4)
+            res["assemble_gbs_into_root"] = round(res["bytes_to_root"] / (asm_ms * 1e-3) / 1e9, 1)
+    res["frame_check"] = a.check(ds)
+    a.close()
+    return res
+
+
+def run_multi(args, c: Ctx, pkg):
+    from opencl_ray_tracer_amd import rowbands
+
+    w, h = args.width, args.height
+    k = args.k if args.k is not None else w / 640.0
+    scene, ds = device_scene(pkg, c, w, h, args.spheres, args.cubes, args.seed, k)
+    rt = pkg.RayTracer(c.gpu)
+    rb, re = rowbands.band_rows(h, c.world, c.rank)
+
+    assemblies = {how: measure_assembly(args, c, pkg, rt, ds, w, h, args.format, how, split=True)
+                  for how in ("rccl_p2p", "xgmi_peer_store")}
+    best, entry = pick_value(assemblies)
+    ms = entry["ms_per_step"]
+
+    # the trace kernel on this rank's band, local stores (the roofline of the
+    # dominant kernel; rank 0's band)
+    band = frame_tensor(c, max(re - rb, 1), w, args.format)
+    step = (rt.bind_render_device(ds, w, h, (rb, re), band.data_ptr(), fmt=args.format,
+                                  stream=c.stream.cuda_stream) if re > rb else (lambda: None))
+    for _ in range(args.warmup):
+        step()
+    rt.profile(True)
+    for _ in range(args.steps):
+        step()
+    prof = rt.profile_read()
+    rt.profile(False)
+    n = max(prof["renders"], 1)
+    trace_ms = prof["trace_ms"] / n
+    band_bytes = BYTES_PER_RAY[args.format] * w * (re - rb)
+    achieved = band_bytes / (trace_ms * 1e-3) / 1e9 if trace_ms > 0 else 0.0
+    del band
+
+    extras = {}
+    if not args.no_extras:
+        # the Texture (RGBA8, MainState.cpp:1023-1037) assembled the same way
+        extras["texture_rgba8"] = {how: measure_assembly(args, c, pkg, rt, ds, w, h, "rgba8", how)
+                                   for how in ("rccl_p2p", "xgmi_peer_store")}
+        # BASELINE config 4: 8192^2, 192 + 64, row-tiled with the assembly
+        c4 = CONFIG4
+        k4 = c4["width"] / 640.0
+        _, ds4 = device_scene(pkg, c, c4["width"], c4["height"], c4["spheres"], c4["cubes"],
+                              c4["seed"], k4)
+        extras["config4"] = {
+            "workload": f"config4: {c4['width']}x{c4['height']} frame, {c4['spheres']} spheres + "
+                        f"{c4['cubes']} cubes, dense k={k4:.1f}, seed {c4['seed']}, "
+                        f"{c.world} row bands (BASELINE names 8 GPUs)",
+            **{how: measure_assembly(args, c, pkg, rt, ds4, c4["width"], c4["height"], "i32x4",
+                                     how) for how in ("rccl_p2p", "xgmi_peer_store")}}
+        del ds4
+        # weak scaling (secondary): a 4096 x 4096N frame with N x (256 + 64)
+        # primitives of the same density, rank r renders rows [4096 r, 4096 (r+1))
+        hw = h * c.world
+        _, dsw = device_scene(pkg, c, w, hw, args.spheres * c.world, args.cubes * c.world,
+                              args.seed, k)
+        outw = frame_tensor(c, h, w, args.format)
+        stepw = rt.bind_render_device(dsw, w, hw, (c.rank * h, (c.rank + 1) * h),
+                                      outw.data_ptr(), fmt=args.format,
+                                      stream=c.stream.cuda_stream)
+        for _ in range(args.warmup):
+            stepw()
+        wms = c.timed(stepw, args.steps)
+        extras["weak_scaling"] = {
+            "workload": f"{w}x{hw} frame, {args.spheres * c.world} spheres + "
+                        f"{args.cubes * c.world} cubes; each rank renders {w}x{h} rows, "
+                        f"no assembly",
+            "ms_per_step": round(wms, 4), "mrays": round(mrays_per_s(w * hw, wms), 1)}
+        del outw, dsw
+
+    rt.close()
+    workload = CONFIG_NAMES.get((w, h, args.spheres, args.cubes), "custom")
+    return {
+        "metric": METRIC, "value": round(mrays_per_s(w * h, ms), 1), "unit": "Mrays/s",
+        "n_gpus": c.world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": f"{workload}: {w}x{h} frame, {args.spheres} spheres + "
+                               f"{args.cubes} cubes, dense k={k:.2f}, seed {args.seed}",
+                   "width": w, "height": h, "spheres": args.spheres, "cubes": args.cubes,
+                   "format": args.format,
+                   "parallelism": f"row-bands x{c.world}, frame assembled on rank 0 by {best}"
+                                  + (" (rehearsal: shared cuda:0, gloo)" if args.rehearse
+                                     else "")},
+        "assembly": assemblies,
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "kernel": "trace3_kernel", "kernel_ms": round(trace_ms, 4),
+                     "algo_bytes_per_launch": band_bytes,
+                     "scope": "rank 0's band, local stores"},
+        **extras,
+        "cpu_baseline": None,
+    }
+
+
+def main():
+    args = parse()
+    c = Ctx(args)
+    pkg = __graft_entry__.load_package()
+    line = run_multi(args, c, pkg) if c.distributed else run_single(args, c, pkg)
+    if c.rank == 0:
+        print(json.dumps(line), flush=True)
+    if c.distributed:
+        c.dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -95,7 +95,8 @@ const char* rt_error_string(int status);
  * [row_begin, row_end) of the width x height frame.
  *   ray_dir       float4, the reference passes (0,0,-1,-1) (MainState.cpp:37-39)
  *   ray_origins   NULL for the reference's implicit (x, y, 0, 1) grid
- *                 (MainState.cpp:44-50), else float4[width*height] (full frame)
+ *                 (MainState.cpp:44-50), else float4[width*height] (full
+ *                 frame; only rows [row_begin, row_end) are uploaded)
  *   host_out      int32[4*width*rows] (I32X4) or uint32[width*rows] (RGBA8)
  *   timing        may be NULL
  * Empty scenes are legal (all pixels (0,0,0,255)). */
@@ -139,6 +140,24 @@ int rt_render_device(rt_ctx* ctx, const rt_scene* device_scene,
                      int32_t width, int32_t height, int32_t row_begin,
                      int32_t row_end, int32_t out_format, int32_t path,
                      void* device_out, void* stream);
+
+/* ---- multi-rank frame assembly over xGMI ------------- */
+/* No reference counterpart (the reference is single-device,
+ * MainState.cpp:1241-1266).  One process per GPU: the root allocates the
+ * whole frame with rt_shared_alloc and hands the 64-byte handle to the
+ * other ranks (any transport, e.g. a broadcast); each rank maps it with
+ * rt_shared_open and passes `mapped + its first row` as rt_render_device's
+ * device_out, so the trace kernel's framebuffer stores travel over xGMI
+ * straight into the root's frame and no separate gather copy exists.
+ * rt_shared_close unmaps an opened frame, rt_shared_free releases the
+ * root's allocation (after every rank has closed it). */
+typedef struct rt_ipc_handle {
+    unsigned char bytes[64];
+} rt_ipc_handle;
+int rt_shared_alloc(rt_ctx* ctx, int64_t bytes, void** device_ptr, rt_ipc_handle* handle);
+int rt_shared_open(rt_ctx* ctx, const rt_ipc_handle* handle, void** device_ptr);
+int rt_shared_close(rt_ctx* ctx, void* device_ptr);
+int rt_shared_free(rt_ctx* ctx, void* device_ptr);
 
 /* Per-kernel HIP-event profiling of rt_render_device / rt_render launches.
  * rt_profile_enable(ctx, 1) starts recording; rt_profile_read synchronises,

@@ -44,7 +44,7 @@ EXPORTED_SYMBOLS = (
     "rt_cube_init", "rt_cube_scale", "rt_cube_rotate", "rt_cube_translate",
     "rt_deg_to_rad", "rt_primary_ray_dir", "rt_scene_reference", "rt_scene_synthetic",
     "rt_pack_rgba8", "rt_abi_version", "rt_cube_build_device", "rt_scene_synthetic_device",
-    "rt_render_multi",
+    "rt_render_multi", "rt_shared_alloc", "rt_shared_open", "rt_shared_close", "rt_shared_free",
 )
 
 
@@ -72,6 +72,10 @@ class _Timing(ctypes.Structure):
         ("kernel_us", ctypes.c_double), ("download_us", ctypes.c_double),
         ("path", ctypes.c_int32),
     ]
+
+
+class _IpcHandle(ctypes.Structure):
+    _fields_ = [("bytes", ctypes.c_ubyte * 64)]
 
 
 _LIB: Optional[ctypes.CDLL] = None
@@ -113,6 +117,11 @@ def library() -> ctypes.CDLL:
         "rt_render_multi": (ctypes.c_int, [ctypes.POINTER(vp), i32, ctypes.POINTER(_Scene), vp,
                                            vp, i32, i32, i32, i32, i32, vp,
                                            ctypes.POINTER(_Timing)]),
+        "rt_shared_alloc": (ctypes.c_int, [vp, ctypes.c_int64, ctypes.POINTER(vp),
+                                           ctypes.POINTER(_IpcHandle)]),
+        "rt_shared_open": (ctypes.c_int, [vp, ctypes.POINTER(_IpcHandle), ctypes.POINTER(vp)]),
+        "rt_shared_close": (ctypes.c_int, [vp, vp]),
+        "rt_shared_free": (ctypes.c_int, [vp, vp]),
         "rt_profile_enable": (ctypes.c_int, [vp, ctypes.c_int]),
         "rt_profile_read": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double),
                                            ctypes.POINTER(ctypes.c_double),
@@ -317,6 +326,8 @@ def render_multi(tracers, scene: Scene, width: int, height: int,
     rb, re = rows if rows is not None else (0, height)
     d = primary_ray_dir() if ray_dir is None else np.ascontiguousarray(ray_dir, np.float32)
     org = None if ray_origins is None else np.ascontiguousarray(ray_origins, np.float32)
+    if org is not None and org.size != 4 * width * height:
+        raise ValueError("ray_origins must hold width*height float4")
     shape = (re - rb, width, 4) if fmt == "i32x4" else (re - rb, width)
     out = np.empty(shape, np.int32 if fmt == "i32x4" else np.uint32)
     ctxs = (ctypes.c_void_p * len(tracers))(*[t.handle.value for t in tracers])
@@ -427,6 +438,32 @@ class RayTracer:
                 _check(rc, "rt_render_device")
         render._keep = keep  # type: ignore[attr-defined]
         return render
+
+    def shared_alloc(self, nbytes: int) -> Tuple[int, bytes]:
+        """rt_shared_alloc: a device buffer on this context's GPU plus the
+        64-byte IPC handle other ranks map it with.  Returns (ptr, handle)."""
+        p, h = ctypes.c_void_p(), _IpcHandle()
+        _check(library().rt_shared_alloc(self._ctx, nbytes, ctypes.byref(p), ctypes.byref(h)),
+               "rt_shared_alloc")
+        return p.value, bytes(h.bytes)
+
+    def shared_open(self, handle: bytes) -> int:
+        """rt_shared_open: map another process's rt_shared_alloc buffer into
+        this context's device (peer access over xGMI)."""
+        if len(handle) != 64:
+            raise ValueError("an IPC handle is 64 bytes")
+        h = _IpcHandle()
+        ctypes.memmove(h.bytes, handle, 64)
+        p = ctypes.c_void_p()
+        _check(library().rt_shared_open(self._ctx, ctypes.byref(h), ctypes.byref(p)),
+               "rt_shared_open")
+        return p.value
+
+    def shared_close(self, ptr: int) -> None:
+        _check(library().rt_shared_close(self._ctx, ptr), "rt_shared_close")
+
+    def shared_free(self, ptr: int) -> None:
+        _check(library().rt_shared_free(self._ctx, ptr), "rt_shared_free")
 
     def profile(self, enable: bool) -> None:
         _check(library().rt_profile_enable(self._ctx, int(enable)), "rt_profile_enable")

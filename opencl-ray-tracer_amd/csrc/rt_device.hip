@@ -480,8 +480,8 @@ __global__ void __launch_bounds__(kThreads) generic_kernel(
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         const int x = (int)(i % width);
         const int y = row_begin + (int)(i / width);
-        const float4 o = origins ? origins[(int64_t)y * width + x]
-                                 : make_float4((float)x, (float)y, 0.0f, 1.0f);
+        // `origins` starts at row row_begin (the band's rows only)
+        const float4 o = origins ? origins[i] : make_float4((float)x, (float)y, 0.0f, 1.0f);
         const int4v p = collide_generic(scene, o, dir);
         if (out_format == RT_FORMAT_I32X4)
             reinterpret_cast<int4v*>(out)[i] = p;
@@ -1706,11 +1706,14 @@ int rt_render_path(rt_ctx* ctx, const rt_scene* scene, const float ray_dir[4],
         HIP_TRY(hipMemcpyAsync(sb + o_cc, scene->cube_colours, 16 * nc, hipMemcpyHostToDevice, st));
     }
     const float* d_origins = nullptr;
-    if (ray_origins) {  // the reference uploads all W*H origins (MainState.cpp:841-855)
-        const size_t ob = (size_t)width * height * 16;
+    if (ray_origins) {
+        // the reference uploads all W*H origins (MainState.cpp:841-855); a
+        // band needs only its own rows
+        const size_t ob = px * 16;
         rc = ensure(&ctx->origin_buf, &ctx->origin_cap, ob);
         if (rc) return rc;
-        HIP_TRY(hipMemcpyAsync(ctx->origin_buf, ray_origins, ob, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(ctx->origin_buf, ray_origins + (size_t)4 * width * row_begin, ob,
+                               hipMemcpyHostToDevice, st));
         d_origins = static_cast<const float*>(ctx->origin_buf);
     }
     rt_scene dscene = *scene;
@@ -1796,8 +1799,56 @@ int rt_render_device(rt_ctx* ctx, const rt_scene* device_scene, const float ray_
     if (path < RT_PATH_AUTO || path > RT_PATH_GENERIC) return RT_ERR_INVALID_ARG;
     HIP_TRY(hipSetDevice(ctx->device));
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
-    return launch(ctx, device_scene, ray_dir, device_ray_origins, width, row_begin, row_end,
+    // launch() reads origins from the band's first row
+    const float* band_origins =
+        device_ray_origins ? device_ray_origins + (size_t)4 * width * row_begin : nullptr;
+    return launch(ctx, device_scene, ray_dir, band_origins, width, row_begin, row_end,
                   out_format, path, device_out, st, nullptr);
+}
+
+int rt_shared_alloc(rt_ctx* ctx, int64_t bytes, void** device_ptr, rt_ipc_handle* handle) {
+    if (!ctx || bytes <= 0 || !device_ptr || !handle) return RT_ERR_INVALID_ARG;
+    static_assert(sizeof(hipIpcMemHandle_t) == sizeof(rt_ipc_handle), "IPC handle size");
+    *device_ptr = nullptr;
+    HIP_TRY(hipSetDevice(ctx->device));
+    void* p = nullptr;
+    // its own allocation: an IPC handle names a whole hipMalloc block
+    if (hipMalloc(&p, (size_t)bytes) != hipSuccess) return RT_ERR_OUT_OF_MEMORY;
+    hipIpcMemHandle_t h;
+    if (hipIpcGetMemHandle(&h, p) != hipSuccess) {
+        (void)hipFree(p);
+        return RT_ERR_HIP;
+    }
+    std::memcpy(handle->bytes, &h, sizeof h);
+    *device_ptr = p;
+    return RT_OK;
+}
+
+int rt_shared_open(rt_ctx* ctx, const rt_ipc_handle* handle, void** device_ptr) {
+    if (!ctx || !handle || !device_ptr) return RT_ERR_INVALID_ARG;
+    *device_ptr = nullptr;
+    HIP_TRY(hipSetDevice(ctx->device));
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, handle->bytes, sizeof h);
+    // mapped for this context's device (peer access over xGMI when the
+    // allocation lives on another GPU)
+    HIP_TRY(hipIpcOpenMemHandle(device_ptr, h, hipIpcMemLazyEnablePeerAccess));
+    return RT_OK;
+}
+
+int rt_shared_close(rt_ctx* ctx, void* device_ptr) {
+    if (!ctx || !device_ptr) return RT_ERR_INVALID_ARG;
+    HIP_TRY(hipSetDevice(ctx->device));
+    HIP_TRY(hipIpcCloseMemHandle(device_ptr));
+    return RT_OK;
+}
+
+int rt_shared_free(rt_ctx* ctx, void* device_ptr) {
+    if (!ctx || !device_ptr) return RT_ERR_INVALID_ARG;
+    HIP_TRY(hipSetDevice(ctx->device));
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipFree(device_ptr));
+    return RT_OK;
 }
 
 int rt_profile_enable(rt_ctx* ctx, int enable) {

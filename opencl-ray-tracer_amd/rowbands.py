@@ -85,6 +85,93 @@ def gather_frame(band: "torch.Tensor", height: int, world: int, rank: int, root:
     return torch.cat(parts)
 
 
+def assemble_frame(frame: Optional["torch.Tensor"], band: "torch.Tensor", height: int,
+                   world: int, rank: int, root: int = 0, group=None, async_op: bool = False):
+    """Assemble the frame on `root` by point-to-point transfers straight
+    into the root's frame rows (RCCL P2P over xGMI with backend "nccl").
+
+    `frame` is the root's whole frame (None elsewhere); the root renders its
+    own band directly into frame[band_rows(root)], so nothing of it moves.
+    Every other rank sends its band, which lands in frame[rb:re] with no
+    padding, staging list or concatenation on the root (unlike
+    gather_frame).  Empty bands (height < world) send nothing.  With
+    async_op the requests are returned (wait() orders the caller's stream
+    after them, without a host sync)."""
+    import torch.distributed as dist
+
+    ops = []
+    if rank == root:
+        for r in range(world):
+            rb, re = band_rows(height, world, r)
+            if r != root and re > rb:
+                ops.append(dist.P2POp(dist.irecv, frame[rb:re], r, group))
+    elif band.shape[0]:
+        ops.append(dist.P2POp(dist.isend, band, root, group))
+    reqs = dist.batch_isend_irecv(ops) if ops else []
+    if async_op:
+        return reqs
+    for q in reqs:
+        q.wait()
+    return None
+
+
+class SharedFrame:
+    """The root's frame mapped into every rank's device (xGMI peer stores).
+
+    The root allocates the whole frame with rt_shared_alloc and broadcasts
+    its 64-byte IPC handle; every other rank maps it with rt_shared_open.
+    rank r then renders its band with `ptr_of_row(rb)` as the device output,
+    so the trace kernel's stores land in the root's HBM and no gather copy
+    runs.  `handle_device` is where the handle tensor lives for the
+    broadcast (the GPU for RCCL, the CPU for gloo)."""
+
+    def __init__(self, tracer, nbytes: int, row_bytes: int, rank: int, root: int = 0,
+                 group=None, handle_device="cpu"):
+        import torch
+        import torch.distributed as dist
+
+        self.tracer, self.rank, self.root = tracer, rank, root
+        self.row_bytes = row_bytes
+        self.owner = rank == root
+        ok = torch.ones(1, dtype=torch.int32, device=handle_device)
+        h = torch.zeros(64, dtype=torch.uint8, device=handle_device)
+        self.ptr = 0
+        self.error: Optional[str] = None
+        if self.owner:
+            try:
+                self.ptr, hb = tracer.shared_alloc(nbytes)
+                h.copy_(torch.frombuffer(bytearray(hb), dtype=torch.uint8))
+            except Exception as e:  # reported, and every rank skips the path
+                self.error = f"rank {rank}: {e}"
+                ok.zero_()
+        dist.broadcast(h, root, group=group)
+        if not self.owner:
+            try:
+                self.ptr = tracer.shared_open(bytes(h.cpu().numpy().tobytes()))
+            except Exception as e:
+                self.error = f"rank {rank}: {e}"
+                ok.zero_()
+        # every rank learns whether all of them hold a mapping
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
+        self.ok = bool(int(ok.item()))
+        if not self.ok and self.error is None:
+            self.error = "another rank could not allocate or map the frame"
+
+    def ptr_of_row(self, row: int) -> int:
+        return self.ptr + row * self.row_bytes
+
+    def close(self, group=None) -> None:
+        """Unmap on every rank, then (after a barrier) free on the root."""
+        import torch.distributed as dist
+
+        if self.ptr and not self.owner:
+            self.tracer.shared_close(self.ptr)
+        dist.barrier(group=group)
+        if self.ptr and self.owner:
+            self.tracer.shared_free(self.ptr)
+        self.ptr = 0
+
+
 def interleaved_blocks(height: int, world: int, rank: int, block: int = 64) -> List[Tuple[int, int]]:
     """Row blocks of `block` rows dealt round-robin over the ranks (SURVEY.md
     §8e: for scenes whose load is not uniform down the frame).  64 rows is
@@ -143,5 +230,11 @@ def render_distributed(render_band: Callable[[int, int], "torch.Tensor"], height
         return gather_frame_interleaved(blocks, height, world, rank, interleave, root=root,
                                         group=group)
     rb, re = band_rows(height, world, rank)
-    band = render_band(rb, re)
+    if re > rb:
+        band = render_band(rb, re)
+    else:
+        # height < world: this rank has no rows.  It renders nothing (an
+        # empty row range is not a legal render) and still joins the gather
+        # with a padded empty band, so no rank blocks in the collective.
+        band = render_band(0, 1)[:0]
     return gather_frame(band, height, world, rank, root=root, group=group)

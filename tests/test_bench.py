@@ -1,0 +1,159 @@
+"""bench.py's arithmetic and the N>1 frame assembly, on the CPU.
+
+The assembly test runs the same rowbands.assemble_frame the GPU bench uses
+(RCCL point-to-point there) over gloo with world sizes 2 and 3, bands of
+unequal size and an empty band, and checks the root's frame row for row."""
+import importlib.util
+import os
+import socket
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+REPO = Path(__file__).resolve().parents[1]
+
+
+def _bench():
+    import __graft_entry__
+    __graft_entry__.load_package()
+    spec = importlib.util.spec_from_file_location("rt_bench", REPO / "bench.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def test_bench_arithmetic():
+    b = _bench()
+    # 4096^2 rays in 0.0584 ms
+    assert b.mrays_per_s(4096 * 4096, 0.0584) == pytest.approx(16777216 / 58.4, rel=1e-12)
+    # every band but the root's reaches the root
+    assert b.bytes_to_root(4096, 4096, 1, "i32x4") == 0
+    assert b.bytes_to_root(4096, 4096, 8, "i32x4") == 16 * 4096 * 4096 * 7 // 8
+    assert b.bytes_to_root(4096, 4096, 8, "rgba8") == 4 * 4096 * 4096 * 7 // 8
+    assert b.bytes_to_root(640, 97, 2, "i32x4") == 16 * 640 * (97 - 48)
+    # value = the fastest assembly whose frame is bit-exact
+    asm = {"rccl_p2p": {"ms_per_step": 0.9, "frame_check": "bit-exact"},
+           "xgmi_peer_store": {"ms_per_step": 0.5, "frame_check": "bit-exact"}}
+    assert b.pick_value(asm)[0] == "xgmi_peer_store"
+    asm["xgmi_peer_store"]["frame_check"] = "MISMATCH"
+    assert b.pick_value(asm)[0] == "rccl_p2p"
+    asm["rccl_p2p"] = {"ms_per_step": None, "error": "no mapping"}
+    with pytest.raises(RuntimeError):
+        b.pick_value(asm)
+
+
+def test_cpu_threads_report(monkeypatch):
+    b = _bench()
+    aff = len(os.sched_getaffinity(0))
+    monkeypatch.setenv("OMP_NUM_THREADS", "3")
+    n, info = b.cpu_threads(0)
+    assert n == min(3, aff)
+    assert info["affinity_cpus"] == aff and info["os_cpu_count"] == os.cpu_count()
+    monkeypatch.delenv("OMP_NUM_THREADS")
+    assert b.cpu_threads(0)[0] == aff
+    assert b.cpu_threads(1)[0] == 1
+
+
+def test_bench_parse_defaults():
+    b = _bench()
+    a = b.parse([])
+    assert (a.gpus, a.width, a.height, a.spheres, a.cubes, a.seed, a.format) == \
+        (1, 4096, 4096, 256, 64, 3, "i32x4")
+    assert b.CONFIG_NAMES[(a.width, a.height, a.spheres, a.cubes)] == "config3"
+    c4 = b.CONFIG4
+    assert b.CONFIG_NAMES[(c4["width"], c4["height"], c4["spheres"], c4["cubes"])] == "config4"
+
+
+def _assemble_worker(rank, world, port, height, width, result_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, str(REPO))
+    import torch
+    import torch.distributed as dist
+
+    import __graft_entry__
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        __graft_entry__.load_package()
+        from opencl_ray_tracer_amd import rowbands
+
+        rb, re = rowbands.band_rows(height, world, rank) if height >= world else \
+            (min(rank, height), min(rank + 1, height))
+
+        def rows(a, b):  # pixel (y, x, c) = 1000 y + 10 x + c, this rank's rows
+            y = torch.arange(a, b, dtype=torch.int32).view(-1, 1, 1)
+            x = torch.arange(width, dtype=torch.int32).view(1, -1, 1)
+            ch = torch.arange(4, dtype=torch.int32).view(1, 1, -1)
+            return (1000 * y + 10 * x + ch).contiguous()
+
+        frame = None
+        if rank == 0:
+            frame = torch.full((height, width, 4), -7, dtype=torch.int32)
+            frame[rb:re] = rows(rb, re)  # the root renders its band in place
+            band = frame[rb:re]
+        else:
+            band = rows(rb, re)
+        rowbands.assemble_frame(frame, band, height, world, rank)
+        if rank == 0:
+            np.save(result_path, frame.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,height", [(2, 97), (3, 100), (3, 7)])
+def test_assemble_frame_gloo(tmp_path, world, height):
+    import torch.multiprocessing as mp
+
+    width = 33
+    out = tmp_path / "frame.npy"
+    mp.spawn(_assemble_worker, args=(world, _free_port(), height, width, str(out)),
+             nprocs=world, join=True)
+    frame = np.load(out)
+    y = np.arange(height).reshape(-1, 1, 1)
+    x = np.arange(width).reshape(1, -1, 1)
+    ch = np.arange(4).reshape(1, 1, -1)
+    assert np.array_equal(frame, 1000 * y + 10 * x + ch)
+
+
+def _empty_band_worker(rank, world, port, result_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, str(REPO))
+    import torch
+    import torch.distributed as dist
+
+    import __graft_entry__
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        __graft_entry__.load_package()
+        from opencl_ray_tracer_amd import rowbands
+
+        def render_band(rb, re):
+            if re <= rb:
+                raise AssertionError("an empty row range must not be rendered")
+            return torch.arange(rb, re, dtype=torch.int32).view(-1, 1).repeat(1, 5)
+
+        frame = rowbands.render_distributed(render_band, 2, world, rank)
+        if rank == 0:
+            np.save(result_path, frame.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_render_distributed_more_ranks_than_rows(tmp_path):
+    """height < world: the rank without rows still joins the gather (no hang)."""
+    import torch.multiprocessing as mp
+
+    out = tmp_path / "frame.npy"
+    mp.spawn(_empty_band_worker, args=(3, _free_port(), str(out)), nprocs=3, join=True)
+    assert np.array_equal(np.load(out), np.array([[0] * 5, [1] * 5]))

@@ -1,0 +1,147 @@
+"""GPU parity at BASELINE's full-size multi-GPU configs, the explicit-origin
+band upload, and the N>1 bench assemblies (rehearsed on one GPU).
+
+Config 4 (8192^2, 192 spheres + 64 cubes, seed 4, dense) and config 5
+(16384^2, 4096 spheres, seed 5, dense k = 25.6: about 11 spheres over each
+pixel, the depth-cull-heavy regime) are rendered WHOLE on the device; a
+deterministic row sample is compared bit-exactly with the oracle, and the
+frame is compared with the 8 row bands the 8-rank layout renders
+(rowbands.band_rows), so the assembled frame of an 8-GPU run is the one-GPU
+frame."""
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REPO = Path(__file__).resolve().parents[1]
+THREADS = min(16, os.cpu_count() or 1)
+
+
+def _device_scene(torch, scene, dev):
+    t = {k: torch.from_numpy(np.ascontiguousarray(getattr(scene, k))).to(dev)
+         for k in ("sphere_origins", "sphere_radius", "sphere_colours", "cube_vertices",
+                   "cube_colours")}
+    ds = {k: v.data_ptr() for k, v in t.items()}
+    ds.update(num_spheres=scene.num_spheres, num_cubes=scene.num_cubes)
+    return t, ds
+
+
+def _full_frame_vs_oracle(pkg, rt, oracle, w, h, ns, nc, seed, rows, bands):
+    torch = pytest.importorskip("torch")
+    from opencl_ray_tracer_amd.rowbands import band_rows
+
+    dev = torch.device("cuda:0")
+    scene = pkg.Scene.synthetic(w, h, ns, nc, seed=seed, k=w / 640)
+    keep, ds = _device_scene(torch, scene, dev)
+    stream = torch.cuda.current_stream().cuda_stream
+    frame = torch.empty((h, w, 4), dtype=torch.int32, device=dev)
+    rt.render_device(ds, w, h, (0, h), frame.data_ptr(), stream=stream)
+    torch.cuda.synchronize()
+    got = frame[torch.tensor(rows, device=dev)].cpu().numpy()
+    want = oracle.trace_rows(scene, w, h, rows, threads=THREADS)
+    for i, r in enumerate(rows):
+        bad = int((got[i] != want[i]).any(-1).sum())
+        assert bad == 0, f"row {r}: {bad} pixels differ"
+    # the row bands of an n-rank run, each a band render, assemble to the frame
+    band = torch.empty_like(frame[: (h + bands - 1) // bands])
+    for r in range(bands):
+        rb, re = band_rows(h, bands, r)
+        rt.render_device(ds, w, h, (rb, re), band.data_ptr(), stream=stream)
+        torch.cuda.synchronize()
+        assert torch.equal(band[: re - rb], frame[rb:re]), f"band {r} ({rb}..{re})"
+    del frame, band, keep
+
+
+def test_config4_full_frame(pkg, rt, oracle):
+    """BASELINE config 4 at full size: 8192^2, 192 spheres + 64 cubes."""
+    h = 8192
+    rows = sorted({0, 1, 63, 64, 1023, 1024, h - 1} | set(range(17, h, 331)))
+    _full_frame_vs_oracle(pkg, rt, oracle, 8192, h, 192, 64, 4, rows, bands=8)
+
+
+def test_config5_full_frame(pkg, rt, oracle):
+    """BASELINE config 5 at full size and density: 16384^2, 4096 spheres,
+    k = 25.6 (about 11 spheres over each pixel: the depth-culled walk)."""
+    h = 16384
+    rows = sorted({0, 2047, 2048, 8192, h - 1} | set(range(331, h, 16384 // 20)))
+    _full_frame_vs_oracle(pkg, rt, oracle, 16384, h, 4096, 0, 5, rows, bands=8)
+
+
+def test_render_multi_explicit_origins_band_upload(pkg, rt, oracle):
+    """rt_render_multi with explicit origins: each band uploads only its own
+    rows of the origin array (MainState.cpp:841-855 uploads them all) and
+    the frame equals the single-context one and the oracle."""
+    rng = np.random.default_rng(11)
+    w, h = 160, 97
+    scene = pkg.Scene.synthetic(w, h, 20, 8, seed=11, k=0.4)
+    d = np.array([0.1, -0.2, -1.0, -1.0], np.float32)
+    org = np.zeros((h, w, 4), np.float32)
+    org[..., 0] = np.arange(w)[None, :] + rng.uniform(-0.5, 0.5, (h, w))
+    org[..., 1] = np.arange(h)[:, None] + rng.uniform(-0.5, 0.5, (h, w))
+    org[..., 2] = rng.uniform(-3, 3, (h, w))
+    org[..., 3] = 1.0
+    full, t = rt.render(scene, w, h, ray_dir=d, ray_origins=org)
+    assert t.path == "generic"
+    assert np.array_equal(full, oracle.trace(scene, w, h, ray_dir=d, ray_origins=org))
+    band, _ = rt.render(scene, w, h, rows=(40, 61), ray_dir=d, ray_origins=org)
+    assert np.array_equal(band, full[40:61])
+    tracers = [rt] + [pkg.RayTracer(0) for _ in range(2)]
+    try:
+        got, times = pkg.render_multi(tracers, scene, w, h, ray_dir=d, ray_origins=org)
+        assert all(tt.path == "generic" for tt in times)
+        assert np.array_equal(got, full)
+        with pytest.raises(ValueError):
+            pkg.render_multi(tracers, scene, w, h, ray_dir=d, ray_origins=org[:-1])
+    finally:
+        for tr in tracers[1:]:
+            tr.close()
+
+
+def test_device_origins_band(pkg, rt, oracle):
+    """rt_render_device with full-frame device origins and a row band reads
+    the band's own rows of them."""
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda:0")
+    w, h = 128, 90
+    scene = pkg.Scene.synthetic(w, h, 16, 6, seed=12, k=0.5)
+    ys, xs = np.mgrid[0:h, 0:w]
+    org = np.stack([xs + 0.25, ys - 0.25, np.zeros_like(xs), np.ones_like(xs)],
+                   -1).astype(np.float32)
+    keep, ds = _device_scene(torch, scene, dev)
+    dorg = torch.from_numpy(org).to(dev)
+    out = torch.empty((30, w, 4), dtype=torch.int32, device=dev)
+    rt.render_device(ds, w, h, (50, 80), out.data_ptr(), origins_ptr=dorg.data_ptr(),
+                     stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    want = oracle.trace(scene, w, h, rows=(50, 80), ray_origins=org)
+    assert np.array_equal(out.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("world", [2])
+def test_bench_rehearsal_assemblies(world, tmp_path):
+    """bench.py at N>1 (rehearsal: every rank on cuda:0, gloo): both frame
+    assemblies -- RCCL-style point-to-point into rank 0's frame, and the
+    peer-store path through an IPC-mapped rank-0 frame (rt_shared_open) --
+    produce a frame bit-identical to a one-GPU render, and the line carries
+    the strong-scaling fields."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={world}", "--master-addr=127.0.0.1", "--master-port=29533",
+           str(REPO / "bench.py"), "--gpus", str(world), "--rehearse", "--steps", "3",
+           "--warmup", "1", "--width", "1024", "--height", "512"]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=tmp_path)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = json.loads([s for s in p.stdout.splitlines() if s.startswith("{")][-1])
+    assert line["n_gpus"] == world and line["scaling"] == "strong"
+    for how in ("rccl_p2p", "xgmi_peer_store"):
+        assert line["assembly"][how]["frame_check"] == "bit-exact", line["assembly"]
+        assert line["texture_rgba8"][how]["frame_check"] == "bit-exact"
+        assert line["config4"][how]["frame_check"] == "bit-exact"
+    assert line["value"] == pytest.approx(1024 * 512 / (line["ms_per_step"] * 1e-3) / 1e6,
+                                          rel=2e-3)
