@@ -63,6 +63,10 @@ int rt_debug_set_bin_masks(rt_ctx* ctx, int enable);
  * tile wave classifies its candidates itself, no coarse kernel), 0 = the
  * general prep -> coarse -> trace path. */
 int rt_debug_set_small_path(rt_ctx* ctx, int enable);
+/* Coarse depth cull of sphere candidates in coarse bins with at least
+ * `enable` sphere candidates (1 = every bin, 0 = off: every candidate the tile
+ * classifier keeps stays; negative = the build's default; A/B and tests). */
+int rt_debug_set_coarse_cull(rt_ctx* ctx, int enable);
 
 /* Host evaluation of the device's restatement of glibc 2.35 sinf / cosf
  * (the same __host__ __device__ code rt_cube_build_device runs), for the

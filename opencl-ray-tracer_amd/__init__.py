@@ -148,6 +148,7 @@ def library() -> ctypes.CDLL:
         "rt_debug_set_list_budget": (ctypes.c_int, [vp, ctypes.c_int64]),
         "rt_debug_set_bin_masks": (ctypes.c_int, [vp, ctypes.c_int]),
         "rt_debug_set_small_path": (ctypes.c_int, [vp, ctypes.c_int]),
+        "rt_debug_set_coarse_cull": (ctypes.c_int, [vp, ctypes.c_int]),
         "rt_cube_build_device": (ctypes.c_int, [vp, vp, vp, i32, vp, vp, vp]),
         "rt_scene_synthetic_device": (ctypes.c_int, [vp, i32, i32, i32, i32, ctypes.c_uint64,
                                                      f32, vp, vp, vp, vp, vp, vp]),
@@ -489,6 +490,13 @@ class RayTracer:
         general prep -> coarse -> trace path (diagnostics / tests)."""
         _check(library().rt_debug_set_small_path(self._ctx, int(enable)),
                "rt_debug_set_small_path")
+
+    def set_coarse_cull(self, min_candidates) -> None:
+        """Diagnostics: the coarse kernel's depth cull of sphere candidates,
+        in bins with at least `min_candidates` candidates (True = every bin,
+        False / 0 = off: every candidate the tile classifier keeps stays)."""
+        _check(library().rt_debug_set_coarse_cull(self._ctx, int(min_candidates)),
+               "rt_debug_set_coarse_cull")
 
     def set_bin_masks(self, enable: bool) -> None:
         """Diagnostics: coarse binning from the separable bin masks (default)

@@ -784,6 +784,9 @@ static_assert(kTiles <= 16 && kTmWords <= 4, "tile words");
 #define RT_C3_ABL 0  // diagnostics only: 1 = box scan + compaction, nothing classified or listed;
                      // 2 = as 1, every wave reading the same 64 boxes (L1-resident)
 #endif
+#ifndef RT_COARSE_CULL
+#define RT_COARSE_CULL 10  // default of rt_debug_set_coarse_cull: bins with >= 10 sphere candidates
+#endif
 #ifndef RT_C3_ROUND
 #define RT_C3_ROUND 64
 #endif
@@ -791,13 +794,80 @@ static_assert(kTiles <= 16 && kTmWords <= 4, "tile words");
 #define RT_C3_BATCH 8
 #endif
 constexpr int kRound = RT_C3_ROUND;
+static_assert(kTmWords == 1, "coarse depth cull: one tile word per candidate");
+
+// Coarse depth cull (`cull`): an upper bound on every pixel's final closest
+// per wave tile, from the spheres that provably hit the WHOLE tile.  The
+// trace computes, per pixel, dist2 = ((lx*lx + ly*ly) + kzw) - tca2 with
+// lx = cx - x, ly = cy - y, then t0 = tca - sqrtf(r2 - dist2) (test_sph);
+// every step is monotone under IEEE rounding, and |lx|, |ly| are largest at
+// a tile edge, so the same operations on the tile's extreme |lx|, |ly| give
+// dist2max >= dist2 and T = tca - sqrtf(r2 - dist2max) >= t0 at every pixel
+// of the tile (exactly, no margin).  If dist2max <= r2 every pixel hits
+// the sphere, and if t0 != 0 is guaranteed too (T < 0, or prep's lower
+// bound tmin > 0) every pixel's closest ends <= T.  A sphere whose lower
+// bound tmin is STRICTLY greater than the tile's smallest T then never wins
+// a pixel of the tile (not even a tie: MainState.cpp:386-391 keeps the
+// first of equal t), so its tile bits are cleared, and a candidate no tile
+// keeps leaves the list.
+// One-sided bounds of the correctly rounded sqrtf (x >= 0): v_sqrt_f32 is
+// within 1 ulp of it on [2^-96, 2^126] (sqrt_rn_normal's +-1 ulp fix-up is
+// exhaustively exact there, scripts/check_sqrt.hip), so +-2 ulp brackets it.
+__device__ __forceinline__ float sqrt_lo_bound(float x) {  // <= sqrtf(x)
+    if (!(x >= 0x1p-96f)) return 0.0f;
+    if (!(x <= 0x1p126f)) return 0x1p63f;
+    return __builtin_bit_cast(float, __builtin_bit_cast(int, __builtin_amdgcn_sqrtf(x)) - 2);
+}
+__device__ __forceinline__ float sqrt_hi_bound(float x) {  // >= sqrtf(x)
+    if (!(x >= 0x1p-96f)) return 0x1p-48f;
+    if (!(x <= 0x1p126f)) return INFINITY;
+    return __builtin_bit_cast(float, __builtin_bit_cast(int, __builtin_amdgcn_sqrtf(x)) + 2);
+}
+
+// Upper bound (order key) of t0 over every pixel of the tile at (tx, ty),
+// when the sphere provably hits all of them with t0 != 0; else ~0u.
+__device__ __forceinline__ unsigned tile_cover_key(const SphRec& r, int tx, int ty) {
+    const float xa = (float)tx, xb = (float)(tx + kWaveTile - 1);
+    const float ya = (float)ty, yb = (float)(ty + kWaveTileH - 1);
+    const float mx = fmaxf(fabsf(r.cx - xa), fabsf(r.cx - xb));
+    const float my = fmaxf(fabsf(r.cy - ya), fabsf(r.cy - yb));
+    const float a = (mx * mx) + (my * my);
+    const float dist2 = (a + r.kzw) - r.tca2;
+    if (!(dist2 <= r.r2)) return 0xffffffffu;  // some pixel may miss (or NaN)
+    const float t = r.tca - sqrt_lo_bound(r.r2 - dist2);
+    const bool nonzero = t < 0.0f || (t == t && r.tmin_key > order_key(0.0f));
+    return nonzero ? order_key(t) : 0xffffffffu;
+}
+
+// Lower bound (order key) of t0 over the pixels of the tile at (tx, ty)
+// that can hit the sphere: the same monotone operations on the tile's
+// smallest |lx|, |ly| (0 when the centre's coordinate lies inside the
+// tile's span) bound dist2 from below, so r2 - dist2 and thc from above.
+// ~0u: no pixel of the tile hits (dist2 > r2 everywhere); 0: no bound.
+__device__ __forceinline__ unsigned tile_low_key(const SphRec& r, int tx, int ty) {
+    const float xa = (float)tx, xb = (float)(tx + kWaveTile - 1);
+    const float ya = (float)ty, yb = (float)(ty + kWaveTileH - 1);
+    const float lxa = r.cx - xa, lxb = r.cx - xb;  // lxa >= lxb
+    const float lya = r.cy - ya, lyb = r.cy - yb;
+    const float mx = (lxa >= 0.0f && lxb <= 0.0f) ? 0.0f : fminf(fabsf(lxa), fabsf(lxb));
+    const float my = (lya >= 0.0f && lyb <= 0.0f) ? 0.0f : fminf(fabsf(lya), fabsf(lyb));
+    const float a = (mx * mx) + (my * my);
+    const float dist2 = (a + r.kzw) - r.tca2;
+    if (dist2 > r.r2) return 0xffffffffu;
+    const float t = r.tca - sqrt_hi_bound(r.r2 - dist2);
+    return t == t ? order_key(t) : 0u;
+}
+
 __global__ void __launch_bounds__(64) coarse3_kernel(
-    const int4* __restrict__ boxes, const Cls* __restrict__ cls, int n_prims, int n_tri,
+    const int4* __restrict__ boxes, const Cls* __restrict__ cls,
+    const SphRec* __restrict__ sph, int n_prims, int n_tri,
     int n_cx, const unsigned long long* __restrict__ row_masks,
     const unsigned long long* __restrict__ col_masks, int row_begin, int half_cap,
-    const unsigned* __restrict__ nonfinite_flag, unsigned gen, int* __restrict__ counts,
-    int* __restrict__ lists) {
+    const unsigned* __restrict__ nonfinite_flag, unsigned gen, int cull_min,
+    int* __restrict__ counts, int* __restrict__ lists) {
     __shared__ int s_ids[kRound];
+    __shared__ SphRec s_sph[kRound];
+    __shared__ unsigned s_tkey[kTiles];  // per tile: smallest cover bound (order key)
     // read early (independent of the scan): a non-finite scene is handed to
     // the trace as count -1, so the trace's first scalar load tells it both
     const bool nonfinite = *nonfinite_flag == gen;
@@ -812,6 +882,9 @@ __global__ void __launch_bounds__(64) coarse3_kernel(
     int* out_tm = out_id + half_cap;
     int count = 0;   // appended to the output
     int staged = 0;  // ids in s_ids
+    if (lane < kTiles) s_tkey[lane] = 0xffffffffu;
+    // the depth cull runs in bins with at least cull_min sphere candidates (0: never)
+    bool cull = false;
     constexpr int kBatch = RT_C3_BATCH;
     auto classify_round = [&](int n) {
         __builtin_amdgcn_wave_barrier();
@@ -823,6 +896,7 @@ __global__ void __launch_bounds__(64) coarse3_kernel(
             for (int w = 0; w < kTmWords; ++w) s_tm[e * kTmWords + w] = 0u;
             s_box[e] = boxes[id];
             s_cls[e] = cls[id];
+            if (cull && id >= n_tri) s_sph[e] = sph[id - n_tri];
         }
         __builtin_amdgcn_wave_barrier();
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
@@ -840,6 +914,10 @@ __global__ void __launch_bounds__(64) coarse3_kernel(
                     pb.w >= ty)
                     classify(s_cls[c], is_tri, (float)tx, (float)ty, &keep, &inside);
                 if (keep) bits = inside ? kTileMask : kKeepMask;
+                if (cull && keep && !is_tri) {
+                    const unsigned key = tile_cover_key(s_sph[c], tx, ty);
+                    if (key != 0xffffffffu) atomicMin(&s_tkey[t], key);
+                }
 #if RT_ROWBITS == 1
                 // a triangle's partial tile: classify each row block
                 if (kBlocks > 1 && is_tri && keep && !inside) {
@@ -908,6 +986,17 @@ __global__ void __launch_bounds__(64) coarse3_kernel(
         for (int c0 = 0; c0 < n_chunks; c0 += 64) {
             const int c = c0 + lane;
             const unsigned long long w = c < n_chunks ? rw[c] & cw[c] : 0ull;
+            if (c0 == 0 && cull_min > 0) {
+                // the gate: sphere candidates (ids >= n_tri) among the first
+                // 4096 primitives, popcounts summed over the wave
+                const int first = n_tri - 64 * c;
+                const unsigned long long sph_bits =
+                    first <= 0 ? ~0ull : first >= 64 ? 0ull : ~0ull << first;
+                int n = __popcll(w & sph_bits);
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1) n += __shfl_xor(n, off);
+                cull = n >= cull_min;
+            }
             unsigned long long nz = __ballot(w != 0ull);
             while (nz) {
                 const int l = __builtin_ctzll(nz);
@@ -919,6 +1008,7 @@ __global__ void __launch_bounds__(64) coarse3_kernel(
             }
         }
     } else {
+        cull = cull_min > 0;  // (count unknown before the scan)
         // scan every box (frames with too many bin rows + columns for masks)
         for (int base = 0; base < n_prims; base += 64 * kBatch) {
             int4 bb[kBatch];
@@ -937,6 +1027,65 @@ __global__ void __launch_bounds__(64) coarse3_kernel(
     }
     if (staged && RT_C3_ABL == 0) classify_round(staged);
     if (RT_C3_ABL != 0 && lane == 0) out_tm[0] = staged;  // keep the scan; lists stay empty
+    // Depth cull (see tile_cover_key): once every candidate of the bin has
+    // been classified, drop each sphere's tiles whose cover bound its tmin
+    // strictly exceeds, and compact the list in place (in order: a kept
+    // entry only moves down, past entries this wave has already read).
+    if (cull && count > 0) {
+        __builtin_amdgcn_wave_barrier();
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        const unsigned own = lane < kTiles ? s_tkey[lane] : 0xffffffffu;
+        if (__ballot(own != 0xffffffffu)) {
+            // the list this wave wrote is read back: its own stores are
+            // ordered before the loads by a workgroup-scope fence (a wave
+            // is its own workgroup here; agent scope would write back L2)
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            int kept = 0;
+            for (int e0 = 0; e0 < count; e0 += 64) {
+                const int n = min(64, count - e0);
+                const int e = e0 + lane;
+                int id = -1;
+                unsigned tm = 0u;
+                if (e < count) {
+                    id = out_id[e];
+                    tm = (unsigned)out_tm[e];
+                    if (id >= n_tri) s_sph[lane] = sph[id - n_tri];
+                }
+                s_ids[lane] = id;
+                s_tm[lane] = tm;
+                __builtin_amdgcn_wave_barrier();
+                __atomic_signal_fence(__ATOMIC_SEQ_CST);
+                // (candidate, tile) pairs over the lanes: a sphere leaves a
+                // tile whose cover bound its tile-local t0 bound exceeds
+                for (int q = lane; q < n * kTiles; q += 64) {
+                    const int c = q / kTiles, t = q % kTiles;
+                    const unsigned tkey = s_tkey[t];
+                    if (s_ids[c] >= n_tri && tkey != 0xffffffffu &&
+                        ((s_tm[c] >> (kTileBits * t)) & 1u)) {
+                        const int tx = x0 + (t % kTilesX) * kWaveTile;
+                        const int ty = y0 + (t / kTilesX) * kWaveTileH;
+                        if (tile_low_key(s_sph[c], tx, ty) > tkey)
+                            atomicAnd(&s_tm[c], ~(kTileMask << (kTileBits * t)));
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
+                __atomic_signal_fence(__ATOMIC_SEQ_CST);
+                tm = s_tm[lane];
+                __builtin_amdgcn_wave_barrier();
+                __atomic_signal_fence(__ATOMIC_SEQ_CST);
+                const bool any = e < count && tm != 0u;
+                const unsigned long long m = __ballot(any);
+                if (any) {
+                    const int pos = kept + (int)__builtin_amdgcn_mbcnt_hi(
+                        (unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+                    out_id[pos] = id;
+                    out_tm[pos] = (int)tm;
+                }
+                kept += __popcll(m);
+            }
+            count = kept;
+        }
+    }
     if (lane == 0) counts[cb] = nonfinite ? -1 : count;
 }
 
@@ -1363,6 +1512,9 @@ struct rt_ctx {
     int64_t list_budget = (int64_t)4 << 30;
     bool bin_masks = RT_BIN_MASKS != 0;  // separable bin masks (false: coarse scans every box)
     bool small_path = true;  // <= 64 x RT_SMALL_CHUNKS primitives: trace_small_kernel
+    // coarse depth cull of sphere candidates in bins with at least this many
+    // candidates (0 = off)
+    int coarse_cull = RT_COARSE_CULL;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     // profiling: per render, start/stop events of the prep, coarse and trace
     // kernels, attached to the kernels' own dispatch packets
@@ -1587,9 +1739,10 @@ int launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origin
                       ctx->flag, ctx->gen, row_masks, col_masks, n_cx, n_cy);
         if (rc) return rc;
         rc = launch_k(coarse3_kernel, dim3((unsigned)n_coarse), dim3(64), stream, pe_coarse,
-                      (const int4*)boxes, (const Cls*)clsv, n_prims, n_tri, n_cx,
-                      (const unsigned long long*)row_masks, (const unsigned long long*)col_masks,
-                      row_begin, half_cap, (const unsigned*)ctx->flag, ctx->gen, counts, lists);
+                      (const int4*)boxes, (const Cls*)clsv, (const SphRec*)sph, n_prims, n_tri,
+                      n_cx, (const unsigned long long*)row_masks,
+                      (const unsigned long long*)col_masks, row_begin, half_cap,
+                      (const unsigned*)ctx->flag, ctx->gen, ctx->coarse_cull, counts, lists);
         if (rc) return rc;
     } else {
         if ((rc = skip_k(ctx, pe_prep))) return rc;
@@ -1941,6 +2094,12 @@ int rt_debug_set_list_budget(rt_ctx* ctx, int64_t bytes) {
 int rt_debug_set_bin_masks(rt_ctx* ctx, int enable) {
     if (!ctx) return RT_ERR_INVALID_ARG;
     ctx->bin_masks = enable != 0;
+    return RT_OK;
+}
+
+int rt_debug_set_coarse_cull(rt_ctx* ctx, int enable) {
+    if (!ctx) return RT_ERR_INVALID_ARG;
+    ctx->coarse_cull = enable < 0 ? RT_COARSE_CULL : enable;  // < 0: the default
     return RT_OK;
 }
 

@@ -1,0 +1,108 @@
+"""Interleaved A/B of one librt_hip.so runtime knob, in ONE process, on the
+BASELINE configs (cdna_hip_programming.md §5.4 rule 24: interleave rounds,
+compare medians).  Each setting's frame must be bit-identical to the first.
+
+    python scripts/ab_knob.py --knob coarse_cull --values 0,1 --configs c3,c5d,c5s,band8
+
+Prints one JSON line per config: median wall us per frame per setting, and
+the per-kernel medians (HIP events on the kernels' dispatch packets).
+"""
+import argparse
+import json
+import statistics
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+REPO = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(REPO))
+
+# name: (width, frame height, rendered rows, spheres, cubes, seed, k)
+CONFIGS = {
+    "c2": (1920, 1080, (0, 1080), 16, 4, 2, 3.0),
+    "c3": (4096, 4096, (0, 4096), 256, 64, 3, 6.4),
+    "c3s": (4096, 4096, (0, 4096), 256, 64, 3, 1.0),
+    "c4": (8192, 8192, (0, 8192), 192, 64, 4, 12.8),
+    "c5d": (16384, 16384, (0, 16384), 4096, 0, 5, 25.6),
+    "c5s": (16384, 16384, (0, 16384), 4096, 0, 5, 1.0),
+    # rank 0's band of bench.py's 8-rank weak-scaling workload
+    "band8": (4096, 32768, (0, 4096), 2048, 512, 3, 6.4),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--knob", default="coarse_cull",
+                    choices=("coarse_cull", "small_path", "bin_masks", "trace_mode"))
+    ap.add_argument("--values", default="0,1")
+    ap.add_argument("--configs", default="c3,c5d,c5s,band8")
+    ap.add_argument("--format", default="i32x4", choices=("i32x4", "rgba8"))
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--steps", type=int, default=10)
+    args = ap.parse_args()
+    import torch
+    import __graft_entry__
+
+    pkg = __graft_entry__.load_package()
+    dev = torch.device("cuda:0")
+    stream = torch.cuda.Stream(dev)
+    rt = pkg.RayTracer(0)
+    setter = {"coarse_cull": rt.set_coarse_cull, "small_path": rt.set_small_path,
+              "bin_masks": rt.set_bin_masks, "trace_mode": rt.set_trace_mode}[args.knob]
+    values = [int(v) for v in args.values.split(",")]
+    for cname in args.configs.split(","):
+        w, h, (rb, re), ns, nc, seed, k = CONFIGS[cname]
+        scene = pkg.Scene.synthetic(w, h, ns, nc, seed=seed, k=k)
+        t = {n: torch.from_numpy(np.ascontiguousarray(getattr(scene, n))).to(dev)
+             for n in ("sphere_origins", "sphere_radius", "sphere_colours", "cube_vertices",
+                       "cube_colours")}
+        ds = {n: v.data_ptr() for n, v in t.items()}
+        ds.update(num_spheres=ns, num_cubes=nc)
+        shape = (re - rb, w, 4) if args.format == "i32x4" else (re - rb, w)
+        out = torch.empty(shape, dtype=torch.int32, device=dev)
+        step = rt.bind_render_device(ds, w, h, (rb, re), out.data_ptr(), fmt=args.format,
+                                     stream=stream.cuda_stream)
+        ref = None
+        for v in values:  # warmup + parity
+            setter(v)
+            for _ in range(3):
+                step()
+            torch.cuda.synchronize()
+            if ref is None:
+                ref = out.clone()
+            elif not torch.equal(out, ref):
+                raise SystemExit(f"{cname}: {args.knob}={v} frame differs from {values[0]}")
+        walls = {v: [] for v in values}
+        kern = {v: {"prep_ms": [], "bin_ms": [], "trace_ms": []} for v in values}
+        for _ in range(args.rounds):
+            for v in values:
+                setter(v)
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for _ in range(args.steps):
+                    step()
+                torch.cuda.synchronize()
+                walls[v].append((time.perf_counter() - t0) * 1e6 / args.steps)
+                rt.profile(True)
+                for _ in range(args.steps):
+                    step()
+                p = rt.profile_read()
+                rt.profile(False)
+                for key in kern[v]:
+                    kern[v][key].append(p[key] * 1e3 / max(p["renders"], 1))
+        res = {"config": cname, "knob": args.knob, "format": args.format,
+               "frame": f"{w}x{h} rows {rb}..{re}, {ns}+{nc}, seed {seed}, k {k}"}
+        for v in values:
+            res[str(v)] = {"wall_us": round(statistics.median(walls[v]), 1),
+                           **{key.replace("_ms", "_us"): round(statistics.median(x), 1)
+                              for key, x in kern[v].items()}}
+        print(json.dumps(res), flush=True)
+        del out, t
+        torch.cuda.empty_cache()
+    rt.close()
+
+
+if __name__ == "__main__":
+    main()

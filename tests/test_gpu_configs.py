@@ -145,3 +145,49 @@ def test_bench_rehearsal_assemblies(world, tmp_path):
         assert line["config4"][how]["frame_check"] == "bit-exact"
     assert line["value"] == pytest.approx(1024 * 512 / (line["ms_per_step"] * 1e-3) / 1e6,
                                           rel=2e-3)
+
+
+def _tie_scene(pkg, w, h, n, seed):
+    """Dense spheres plus exact duplicates (equal t everywhere: the first in
+    order must win, MainState.cpp:386-391) and concentric copies."""
+    rng = np.random.default_rng(seed)
+    so = np.zeros((n, 4), np.float32)
+    so[:, 0] = rng.uniform(0, w, n)
+    so[:, 1] = rng.uniform(0, h, n)
+    so[:, 2] = -rng.uniform(20, 100, n)
+    r = rng.uniform(5, 30, n).astype(np.float32) * (w / 64)
+    sc = np.concatenate([rng.uniform(0.05, 1, (n, 3)), np.full((n, 1), 255)], 1).astype(np.float32)
+    dup = rng.choice(n, n // 8, replace=False)
+    so = np.concatenate([so, so[dup]])
+    r = np.concatenate([r, r[dup]])
+    sc = np.concatenate([sc, sc[dup][:, [2, 0, 1, 3]]])
+    return pkg.Scene(so, r, sc)
+
+
+@pytest.mark.parametrize("case", ["dense", "dense_rgba8", "ties", "cubes_and_spheres"])
+def test_coarse_depth_cull_exact(pkg, rt, oracle, case):
+    """The coarse kernel's depth cull (per-tile cover bounds) drops only
+    spheres that cannot win a pixel: frames with it on and off are
+    identical and equal the oracle, in the dense regime where it drops most
+    and with exact ties."""
+    fmt = "rgba8" if case.endswith("rgba8") else "i32x4"
+    w, h = 640, 480
+    if case == "ties":
+        scene = _tie_scene(pkg, w, h, 400, 3)
+    elif case == "cubes_and_spheres":
+        scene = pkg.Scene.synthetic(w, h, 300, 40, seed=9, k=w / 640 * 4)
+    else:
+        scene = pkg.Scene.synthetic(w, h, 1200, 0, seed=5, k=w / 640 * 4)
+    try:
+        rt.set_coarse_cull(0)
+        off, _ = rt.render(scene, w, h, fmt=fmt)
+        rt.set_coarse_cull(1)  # every bin
+        on, t = rt.render(scene, w, h, fmt=fmt)
+    finally:
+        rt.set_coarse_cull(-1)  # the library default
+    assert t.path == "binned"
+    assert np.array_equal(on, off)
+    want = oracle.trace(scene, w, h, threads=THREADS)
+    if fmt == "rgba8":
+        want = oracle.pack_rgba8(want)
+    assert np.array_equal(on, want)
