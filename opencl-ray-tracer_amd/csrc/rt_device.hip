@@ -599,7 +599,16 @@ __device__ __forceinline__ unsigned rt_now() { return (unsigned)__builtin_amdgcn
 #ifndef RT_ROWSKIP
 #define RT_ROWSKIP 0  // 1: skip triangle rows, 2: sphere rows, 3: both (no lane can hit)
 #endif
+#ifndef RT_ROWSKIP_RGBA8
+#define RT_ROWSKIP_RGBA8 0  // the same for the Texture (RGBA8) trace (1-3 measured slower)
+#endif
+// Row skipping per output format: the int32x4 trace hides its test VALU
+// under the store drain (measured slower with skips), the RGBA8 trace is
+// VALU-bound.
+template <int kFmt>
+constexpr int row_skip() { return kFmt == RT_FORMAT_RGBA8 ? RT_ROWSKIP_RGBA8 : RT_ROWSKIP; }
 
+template <int kSkip = RT_ROWSKIP>
 __device__ __forceinline__ void test_tri(const TriRec& r, int slot, unsigned bits, double px,
                                          const double* py, float* closest, int* hit) {
     const double tx = px - r.v0x;
@@ -620,7 +629,7 @@ __device__ __forceinline__ void test_tri(const TriRec& r, int slot, unsigned bit
             const double v = (r.dz * q2) * r.inv_det;
             pass = !((u < 0.0) | (u > 1.0) | (v < 0.0) | (u + v > 1.0));
             // no lane of this row inside the triangle: its t is never used
-            if ((RT_ROWSKIP & 1) && __ballot(pass) == 0ull) continue;
+            if ((kSkip & 1) && __ballot(pass) == 0ull) continue;
         }
         const double q0 = ty * r.e1z - r.k0;
         const double t = ((r.e2x * q0 + e2yq1) + r.e2z * q2) * r.inv_det;
@@ -645,6 +654,7 @@ __device__ __forceinline__ float sqrt_rn_normal(float x) {
     return r;
 }
 
+template <int kSkip = RT_ROWSKIP>
 __device__ __forceinline__ void test_sph(const SphRec& s, int slot, unsigned bits, float pxf,
                                          const float* pyf, float* closest, int* hit) {
     const float lx = s.cx - pxf;
@@ -664,10 +674,14 @@ __device__ __forceinline__ void test_sph(const SphRec& s, int slot, unsigned bit
     for (int j = 0; j < kRowsPerLane; ++j) {
         if (!((bits >> (2 * row_block(j))) & 1u)) continue;  // block skipped (uniform)
         // no lane of this row within the sphere's disc: nothing to update
-        if ((RT_ROWSKIP & 2) && __ballot(!(dist2[j] > s.r2)) == 0ull) continue;
+        if ((kSkip & 2) && __ballot(!(dist2[j] > s.r2)) == 0ull) continue;
         const float thc = general ? sqrtf(arg[j]) : sqrt_rn_normal(arg[j]);
         const float t0 = s.tca - thc;
-        const bool take = !(dist2[j] > s.r2) & (t0 != 0.0f) & (t0 < closest[j]);
+        // dist2 > r2 (a miss, MainState.cpp:314) makes arg = r2 - dist2 < 0
+        // (the sign of a difference of floats is exact), so thc and t0 are
+        // NaN and `t0 < closest` fails: the miss test needs no compare of
+        // its own.  A NaN dist2 gives a NaN t0 as well.
+        const bool take = (t0 != 0.0f) & (t0 < closest[j]);
         closest[j] = take ? t0 : closest[j];
         hit[j] = take ? slot : hit[j];
     }
@@ -709,14 +723,75 @@ __device__ __forceinline__ void store_fmt(void* __restrict__ out, int64_t idx, i
         reinterpret_cast<unsigned*>(out)[idx] = pack_rgba8(pix);
 }
 
-// Shade (MainState.cpp:396-407) one lane's kRowsPerLane pixels.
-template <int kMode = 0>
+// The same for shade_pixels' output: RGBA8 words arrive packed in pix.x.
+template <int kFmt>
+__device__ __forceinline__ void store_shaded(void* __restrict__ out, int64_t idx, int4v pix) {
+    if (kFmt == RT_FORMAT_I32X4)
+        reinterpret_cast<int4v*>(out)[idx] = pix;
+    else
+        reinterpret_cast<unsigned*>(out)[idx] = (unsigned)pix.x;
+}
+
+// The Texture packing (MainState.cpp:1026-1036) of three (int) channels.
+__device__ __forceinline__ unsigned pack_bytes(int r, int g, int b) {
+    return ((unsigned)r & 0xffu) | (((unsigned)g & 0xffu) << 8) | (((unsigned)b & 0xffu) << 16) |
+           0xFF000000u;
+}
+
+// Shade (MainState.cpp:396-407) one lane's kRowsPerLane pixels.  Int32x4:
+// pix[j] is the pixel.  RGBA8: pix[j].x is the packed Texture word.
+template <int kMode = 0, int kFmt = RT_FORMAT_I32X4>
 __device__ __forceinline__ void shade_pixels(const float4* __restrict__ colours,
                                              const float* closest, const int* hit, int4v* pix) {
     bool lane_hit = false;
 #pragma unroll
     for (int j = 0; j < kRowsPerLane; ++j) lane_hit |= hit[j] >= 0;
     const bool any_hit = __ballot(lane_hit) != 0ull;
+    if (kFmt == RT_FORMAT_RGBA8) {
+        // The Texture keeps the low byte of each (int) channel.  x86's (int)
+        // gives INT32_MIN (low byte 0) for NaN, +-inf and |f| >= 2^31;
+        // v_cvt_i32_f32 agrees on that byte except for f >= 2^31 (it
+        // saturates to 0x7fffffff), so one wave-uniform max3 test replaces
+        // the per-channel fix-ups of cvt_i32_fast on the common path.
+#pragma unroll
+        for (int j = 0; j < kRowsPerLane; ++j) pix[j].x = (int)0xFF000000u;
+        if (!any_hit) return;
+        float4 col[kRowsPerLane];
+#pragma unroll
+        for (int j = 0; j < kRowsPerLane; ++j)
+            col[j] = kMode == 4 ? make_float4(1.0f, 0.5f, 0.25f, 255.0f)
+                                : colours[hit[j] >= 0 ? hit[j] : 0];
+        float f[kRowsPerLane][3];
+        bool big = false;
+#pragma unroll
+        for (int j = 0; j < kRowsPerLane; ++j) {
+            const float normalised = div180(hit[j] >= 0 ? closest[j] : 1.0f);
+            const float scalar = 255.0f - (normalised * 255.0f);
+            f[j][0] = scalar * col[j].x;
+            f[j][1] = scalar * col[j].y;
+            f[j][2] = scalar * col[j].z;
+            big |= !(fmaxf(fmaxf(f[j][0], f[j][1]), f[j][2]) < 2147483648.0f);
+        }
+        if (__ballot(big)) {
+#pragma unroll
+            for (int j = 0; j < kRowsPerLane; ++j) {
+                const unsigned w = pack_bytes(cvt_i32_fast(f[j][0]), cvt_i32_fast(f[j][1]),
+                                              cvt_i32_fast(f[j][2]));
+                pix[j].x = hit[j] >= 0 ? (int)w : pix[j].x;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < kRowsPerLane; ++j) {
+                int c[3];
+#pragma unroll
+                for (int k = 0; k < 3; ++k)
+                    asm volatile("v_cvt_i32_f32 %0, %1" : "=v"(c[k]) : "v"(f[j][k]));
+                const unsigned w = pack_bytes(c[0], c[1], c[2]);
+                pix[j].x = hit[j] >= 0 ? (int)w : pix[j].x;
+            }
+        }
+        return;
+    }
 #pragma unroll
     for (int j = 0; j < kRowsPerLane; ++j) pix[j] = int4v{0, 0, 0, 255};
     if (any_hit) {
@@ -735,9 +810,9 @@ __device__ __forceinline__ void shade_pixels(const float4* __restrict__ colours,
     }
 }
 
-// Store one lane's kRowsPerLane pixels (rows kLaneRows apart) of the wave
-// tile at (tile_x, tile_y), in the Texture format (MainState.cpp:1026-1036)
-// or int32x4.  `full`: the whole tile lies inside the frame band, so no
+// Store one lane's kRowsPerLane shaded pixels (rows kLaneRows apart) of the
+// wave tile at (tile_x, tile_y), in the Texture format (MainState.cpp:
+// 1026-1036, packed by shade_pixels) or int32x4.  `full`: the whole tile lies inside the frame band, so no
 // per-lane bounds checks.
 template <int kMode, int kFmt>
 __device__ __forceinline__ void store_rows(const int4v* pix, int x, int y0, int width,
@@ -750,11 +825,11 @@ __device__ __forceinline__ void store_rows(const int4v* pix, int x, int y0, int 
         // kMode 3: everything but the stores (a store the compiler cannot drop)
         const bool store = kMode != 3 || pix[j].x == 0x7fffffff;
         if (full) {
-            if (store) store_fmt<kFmt>(out, idx0 + j * row_step, pix[j]);
+            if (store) store_shaded<kFmt>(out, idx0 + j * row_step, pix[j]);
         } else {
             const int y = y0 + kLaneRows * j;
             if (x < width && y < row_end && store)
-                store_fmt<kFmt>(out, idx0 + j * row_step, pix[j]);
+                store_shaded<kFmt>(out, idx0 + j * row_step, pix[j]);
         }
     }
 }
@@ -1231,7 +1306,9 @@ __global__ void __launch_bounds__(64 * kTraceWaves) RT_TRACE_ATTR trace3_kernel(
             if (x < width && y < row_end)
                 p = collide_generic(scene, make_float4((float)x, (float)y, 0.0f, 1.0f), dir);
 #if RT_LDS_STORE
-            s_pix[w_self][j][lane] = p;
+            // store_rows stores shaded pixels: RGBA8 words packed in .x
+            s_pix[w_self][j][lane] =
+                kFmt == RT_FORMAT_RGBA8 ? int4v{(int)pack_rgba8(p), 0, 0, 0} : p;
 #else
             if (x < width && y < row_end)
                 store_fmt<kFmt>(out, (int64_t)(y - row_begin) * width + x, p);
@@ -1294,7 +1371,7 @@ __global__ void __launch_bounds__(64 * kTraceWaves) RT_TRACE_ATTR trace3_kernel(
             if (p < n_tri) {
                 const TriRec r = tri[p];
                 asm volatile("" ::"s"(r.p0), "s"(r.p1), "s"(r.dz));
-                test_tri(r, p / 12, bits, px, py, closest, hit);
+                test_tri<row_skip<kFmt>()>(r, p / 12, bits, px, py, closest, hit);
             } else {
                 const SphRec r = sph[p - n_tri];
 #if RT_DEPTH_CULL
@@ -1305,7 +1382,8 @@ __global__ void __launch_bounds__(64 * kTraceWaves) RT_TRACE_ATTR trace3_kernel(
                 }
                 if (r.tmin_key >= tile_max_key) continue;
 #endif
-                test_sph(r, scene.n_cubes + (p - n_tri), bits, pxf, pyf, closest, hit);
+                test_sph<row_skip<kFmt>()>(r, scene.n_cubes + (p - n_tri), bits, pxf, pyf, closest,
+                                           hit);
             }
 #if RT_DEPTH_CULL
             dirty = true;
@@ -1315,10 +1393,11 @@ __global__ void __launch_bounds__(64 * kTraceWaves) RT_TRACE_ATTR trace3_kernel(
 #if RT_TIMELINE
     tl2 = rt_now();
 #endif
-    shade_pixels<kMode>(colours, closest, hit, pix);
+    shade_pixels<kMode, kFmt>(colours, closest, hit, pix);
     } else {  // outside the frame: nothing is stored
 #pragma unroll
-        for (int j = 0; j < kRowsPerLane; ++j) pix[j] = int4v{0, 0, 0, 255};
+        for (int j = 0; j < kRowsPerLane; ++j)
+            pix[j] = int4v{kFmt == RT_FORMAT_RGBA8 ? (int)0xFF000000u : 0, 0, 0, 255};
     }
 #if RT_LDS_STORE
 #pragma unroll
@@ -1461,7 +1540,7 @@ __global__ void __launch_bounds__(64) RT_TRACE_ATTR trace_small_kernel(
         if (p < n_tri) {
             const TriRec r = tri[p];
             asm volatile("" ::"s"(r.p0), "s"(r.p1), "s"(r.dz));
-            test_tri(r, p / 12, bits, px, py, closest, hit);
+            test_tri<row_skip<kFmt>()>(r, p / 12, bits, px, py, closest, hit);
         } else {
             const SphRec r = sph[p - n_tri];
 #if RT_DEPTH_CULL
@@ -1471,13 +1550,13 @@ __global__ void __launch_bounds__(64) RT_TRACE_ATTR trace_small_kernel(
             }
             if (r.tmin_key >= tile_max_key) continue;
 #endif
-            test_sph(r, n_cubes + (p - n_tri), bits, pxf, pyf, closest, hit);
+            test_sph<row_skip<kFmt>()>(r, n_cubes + (p - n_tri), bits, pxf, pyf, closest, hit);
         }
 #if RT_DEPTH_CULL
         dirty = true;
 #endif
     }
-    shade_pixels<0>(colours, closest, hit, pix);
+    shade_pixels<0, kFmt>(colours, closest, hit, pix);
     const bool full = rel_x + kWaveTile <= width && tile_y + kWaveTileH <= row_end;
     store_rows<0, kFmt>(pix, x, y0, width, row_begin, row_end, full, out);
 }

@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--ranks", type=int, default=1,
                     help="render rank 0's band of a frame and scene scaled for this many ranks "
                          "(bench.py's weak-scaling workload)")
+    ap.add_argument("--format", default="i32x4", choices=("i32x4", "rgba8"))
     ap.add_argument("--modes", default="0",
                     help="comma list of trace-kernel ablation modes to time (0 = real)")
     args = ap.parse_args()
@@ -53,7 +54,8 @@ def main():
                     scene.num_cubes, None, 0)
     d = pkg.primary_ray_dir()
     stream = torch.cuda.Stream(dev)
-    out = torch.empty((h, w, 4), dtype=torch.int32, device=dev)
+    fmt = 0 if args.format == "i32x4" else 1
+    out = torch.empty((h, w, 4) if fmt == 0 else (h, w), dtype=torch.int32, device=dev)
     libs = []
     for path in args.libs:
         lib = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
@@ -67,7 +69,7 @@ def main():
     def run(lib, ctx, n):
         for _ in range(n):
             rc = lib.rt_render_device(ctx, ctypes.byref(sc), d.ctypes.data, None, w, full_h, 0,
-                                      h, 0, 0, out.data_ptr(), stream.cuda_stream)
+                                      h, fmt, 0, out.data_ptr(), stream.cuda_stream)
             assert rc == 0
 
     ref = None
