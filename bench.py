@@ -77,7 +77,8 @@ def parse(argv=None):
     ap.add_argument("--no-host-path", action="store_true",
                     help="skip the end-to-end rt_render (host buffers) measurement")
     ap.add_argument("--no-extras", action="store_true",
-                    help="N>1: time only the headline assemblies (no Texture / config 4 / weak)")
+                    help="time only the headline workload (N=1: no RGBA8 Texture line; "
+                         "N>1: no Texture / config 4 / weak-scaling keys)")
     ap.add_argument("--path", choices=("auto", "binned", "generic"), default="auto",
                     help="kernel path: generic = the brute-force per-pixel kernel (every ray "
                          "against every primitive), for the compute-bound comparison")
@@ -277,22 +278,54 @@ def run_single(args, c: Ctx, pkg):
         # through the synchronous host-buffer entry point rt_render.  Never
         # `value`: it includes the PCIe copy of the whole frame.
         host_buf = np.empty(tuple(out.shape), np.int32 if args.format == "i32x4" else np.uint32)
-        runs = [rt.render(scene, w, h, fmt=args.format, out=host_buf)[1] for _ in range(4)][1:]
-        best = min(runs, key=lambda t: t.total_us)
+
+        def host_runs():
+            runs = [rt.render(scene, w, h, fmt=args.format, out=host_buf)[1] for _ in range(4)]
+            best = min(runs[1:], key=lambda t: t.total_us)
+            return {"total_ms": round(best.total_us / 1e3, 3),
+                    "upload_ms": round(best.upload_us / 1e3, 3),
+                    "kernel_ms": round(best.kernel_us / 1e3, 3),
+                    "download_ms": round(best.download_us / 1e3, 3),
+                    "mrays_end_to_end": round(rays / best.total_us, 1)}
         host = {"scope": "rt_render: scene upload + kernels + frame download (PCIe) into a "
-                         "reused host buffer",
-                "total_ms": round(best.total_us / 1e3, 3),
-                "upload_ms": round(best.upload_us / 1e3, 3),
-                "kernel_ms": round(best.kernel_us / 1e3, 3),
-                "download_ms": round(best.download_us / 1e3, 3),
-                "mrays_end_to_end": round(rays / best.total_us, 1)}
+                         "reused host buffer", **host_runs()}
+        # the same into a page-locked buffer (rt_host_register): direct DMA
+        pkg.host_register(host_buf)
+        host["registered"] = host_runs()
+        pkg.host_unregister(host_buf)
+        del host_buf
+
+    # Second workload: the same frame in the Texture's RGBA8 packing
+    # (MainState.cpp:1023-1037, north_star's Texture), 4 B/ray, with its own
+    # roofline.  Timed the same way; never `value`.
+    texture = None
+    if args.format == "i32x4" and not args.no_extras and args.trace_mode == 0:
+        tex = frame_tensor(c, h, w, "rgba8")
+        tstep = rt.bind_render_device(ds, w, h, (0, h), tex.data_ptr(), fmt="rgba8",
+                                      path=args.path, stream=c.stream.cuda_stream)
+        for _ in range(args.warmup):
+            tstep()
+        t_wall = c.timed(tstep, args.steps)
+        rt.profile(True)
+        for _ in range(args.steps):
+            tstep()
+        tp = rt.profile_read()
+        rt.profile(False)
+        t_trace = tp["trace_ms"] / max(tp["renders"], 1)
+        t_bytes = BYTES_PER_RAY["rgba8"] * w * h
+        t_ach = t_bytes / (t_trace * 1e-3) / 1e9
+        texture = {"format": "rgba8", "ms_per_step": round(t_wall, 4),
+                   "value": round(mrays_per_s(w * h, t_wall), 1), "unit": "Mrays/s",
+                   "roofline": {"bound": "hbm", "achieved": round(t_ach, 1), "peak": HBM_PEAK_GBS,
+                                "unit": "GB/s", "frac": round(t_ach / HBM_PEAK_GBS, 4),
+                                "kernel": kernel_name(args), "kernel_ms": round(t_trace, 4),
+                                "algo_bytes_per_launch": t_bytes,
+                                "note": "VALU-issue bound (DESIGN.md §3, profiles/r02/pmc_mix)"}}
+        del tex
 
     cpu = None if args.no_cpu_baseline else cpu_baseline(args, scene, w, h)
     workload = CONFIG_NAMES.get((w, h, args.spheres, args.cubes), "custom")
-    # the dominant kernel: scenes of at most 512 primitives take trace_small_kernel
-    kernel = ("generic_kernel" if args.path == "generic" else
-              "trace_small_kernel" if 0 < args.spheres + 12 * args.cubes <= 512 else
-              "trace3_kernel")
+    kernel = kernel_name(args)
     rt.close()
     return {
         "metric": METRIC, "value": round(mrays_per_s(rays, wall_ms), 1), "unit": "Mrays/s",
@@ -310,9 +343,18 @@ def run_single(args, c: Ctx, pkg):
                      "algo_bytes_per_launch": algo_bytes},
         "event_ms_per_step": round(event_ms, 4),
         "profiled_pass_ms_per_step": round(prof_wall_ms, 4),
+        "texture_rgba8": texture,
         "cpu_baseline": cpu,
         "host_path": host,
     }
+
+
+def kernel_name(args) -> str:
+    """The dominant kernel: scenes of at most 512 primitives take
+    trace_small_kernel."""
+    return ("generic_kernel" if args.path == "generic" else
+            "trace_small_kernel" if 0 < args.spheres + 12 * args.cubes <= 512 else
+            "trace3_kernel")
 
 
 def cpu_baseline(args, scene, w, h):
@@ -485,6 +527,78 @@ def measure_assembly(args, c, pkg, rt, ds, width, height, fmt, how, split=False)
     return res
 
 
+def measure_host_frame(args, c: Ctx, pkg, rt, scene, w, h, fmt="i32x4"):
+    """The reference's own consumer, a host frame (`pixels`, MainState.cpp:
+    215/676, read back at :876-907), filled by N GPUs at once: every rank
+    calls rt_render (the executeRayTracerOpenCL replacement: scene upload,
+    render, download -- the app's timer scope, :662-894) for its band,
+    straight into its rows of ONE page-locked host frame shared by the ranks
+    (POSIX shared memory), each over its own GPU's PCIe link.  A step ends
+    when every rank's rows are in (barrier).  Checked bit-exactly on rank 0
+    against a one-GPU device render."""
+    from multiprocessing import resource_tracker, shared_memory
+
+    from opencl_ray_tracer_amd.rowbands import band_rows
+
+    shape = (h, w, 4) if fmt == "i32x4" else (h, w)
+    nbytes = BYTES_PER_RAY[fmt] * w * h
+    rb, re = band_rows(h, c.world, c.rank)
+    shm = frame = None
+    name = [None]
+    try:
+        if c.rank == 0:
+            shm = shared_memory.SharedMemory(create=True, size=nbytes)
+            name = [shm.name]
+        c.dist.broadcast_object_list(name, 0)
+        if c.rank != 0:
+            shm = shared_memory.SharedMemory(name=name[0])
+            resource_tracker.unregister(shm._name, "shared_memory")  # rank 0 unlinks it
+        frame = np.ndarray(shape, np.int32 if fmt == "i32x4" else np.uint32, buffer=shm.buf)
+        pkg.host_register(frame)
+        band = frame[rb:re]
+
+        def step():
+            if re > rb:
+                rt.render(scene, w, h, rows=(rb, re), fmt=fmt, out=band)
+            c.dist.barrier()
+        for _ in range(max(1, args.warmup)):
+            step()
+        ms = c.timed(step, args.steps)
+        ok = c.torch.ones(1, dtype=c.torch.int32, device=c.coll_dev)
+        if c.rank == 0:
+            keep, ds = device_scene_from(c, scene)
+            ref = frame_tensor(c, h, w, fmt)
+            rt.bind_render_device(ds, w, h, (0, h), ref.data_ptr(), fmt=fmt,
+                                  stream=c.stream.cuda_stream)()
+            c.sync()
+            ok.fill_(int(np.array_equal(ref.cpu().numpy().view(frame.dtype), frame)))
+            del ref, keep
+        c.dist.broadcast(ok, 0)
+        pkg.host_unregister(frame)
+        return {"scope": "rt_render per rank (scene upload + render + band download over its "
+                         "own PCIe link) into one shared page-locked host frame, then a barrier",
+                "format": fmt, "ms_per_step": round(ms, 4),
+                "mrays_end_to_end": round(mrays_per_s(w * h, ms), 1),
+                "host_gbs": round(nbytes / (ms * 1e-3) / 1e9, 1),
+                "frame_check": "bit-exact" if int(ok.item()) else "MISMATCH"}
+    finally:
+        del frame
+        if shm is not None:
+            shm.close()
+            c.dist.barrier()
+            if c.rank == 0:
+                shm.unlink()
+
+
+def device_scene_from(c: Ctx, scene):
+    t = {name: c.torch.from_numpy(np.ascontiguousarray(getattr(scene, name))).to(c.dev)
+         for name in ("sphere_origins", "sphere_radius", "sphere_colours", "cube_vertices",
+                      "cube_colours")}
+    ds = {name: v.data_ptr() for name, v in t.items()}
+    ds.update(num_spheres=scene.num_spheres, num_cubes=scene.num_cubes)
+    return t, ds
+
+
 def run_multi(args, c: Ctx, pkg):
     from opencl_ray_tracer_amd import rowbands
 
@@ -552,6 +666,8 @@ def run_multi(args, c: Ctx, pkg):
                         f"no assembly",
             "ms_per_step": round(wms, 4), "mrays": round(mrays_per_s(w * hw, wms), 1)}
         del outw, dsw
+        # the app's host frame filled by every GPU over its own PCIe link
+        extras["host_frame"] = measure_host_frame(args, c, pkg, rt, scene, w, h)
 
     rt.close()
     workload = CONFIG_NAMES.get((w, h, args.spheres, args.cubes), "custom")

@@ -159,6 +159,14 @@ int rt_shared_open(rt_ctx* ctx, const rt_ipc_handle* handle, void** device_ptr);
 int rt_shared_close(rt_ctx* ctx, void* device_ptr);
 int rt_shared_free(rt_ctx* ctx, void* device_ptr);
 
+/* Page-lock (and unlock) a caller-owned host buffer, e.g. the app's
+ * `pixels` vector (MainState.cpp:215, :676), so that rt_render's frame
+ * download is a direct DMA at the PCIe link rate instead of a staged copy.
+ * Portable: every context / device may use it.  The reference maps and
+ * copies an OpenCL buffer instead (MainState.cpp:876-907). */
+int rt_host_register(void* host_ptr, int64_t bytes);
+int rt_host_unregister(void* host_ptr);
+
 /* Per-kernel HIP-event profiling of rt_render_device / rt_render launches.
  * rt_profile_enable(ctx, 1) starts recording; rt_profile_read synchronises,
  * returns the summed milliseconds of the prep, bin and trace kernels and the

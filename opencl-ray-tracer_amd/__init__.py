@@ -25,7 +25,7 @@ __all__ = [
     "RT_PATH_GENERIC", "RtError", "Scene", "Timing", "RayTracer", "MainState",
     "library", "library_path", "primary_ray_dir", "pack_rgba8", "cube_packed",
     "deg_to_rad", "encode_png", "EXPORTED_SYMBOLS", "CUBE_OP_DTYPE", "cube_ops", "render_multi",
-    "debug_glibc_sincosf",
+    "debug_glibc_sincosf", "host_register", "host_unregister",
 ]
 
 PKG_DIR = Path(__file__).resolve().parent
@@ -45,6 +45,7 @@ EXPORTED_SYMBOLS = (
     "rt_deg_to_rad", "rt_primary_ray_dir", "rt_scene_reference", "rt_scene_synthetic",
     "rt_pack_rgba8", "rt_abi_version", "rt_cube_build_device", "rt_scene_synthetic_device",
     "rt_render_multi", "rt_shared_alloc", "rt_shared_open", "rt_shared_close", "rt_shared_free",
+    "rt_host_register", "rt_host_unregister",
 )
 
 
@@ -122,6 +123,8 @@ def library() -> ctypes.CDLL:
         "rt_shared_open": (ctypes.c_int, [vp, ctypes.POINTER(_IpcHandle), ctypes.POINTER(vp)]),
         "rt_shared_close": (ctypes.c_int, [vp, vp]),
         "rt_shared_free": (ctypes.c_int, [vp, vp]),
+        "rt_host_register": (ctypes.c_int, [vp, ctypes.c_int64]),
+        "rt_host_unregister": (ctypes.c_int, [vp]),
         "rt_profile_enable": (ctypes.c_int, [vp, ctypes.c_int]),
         "rt_profile_read": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double),
                                            ctypes.POINTER(ctypes.c_double),
@@ -340,6 +343,16 @@ def render_multi(tracers, scene: Scene, width: int, height: int,
     names = {RT_PATH_BINNED: "binned", RT_PATH_GENERIC: "generic"}
     return out, [Timing(t.total_us, t.upload_us, t.kernel_us, t.download_us,
                         names.get(t.path, "idle")) for t in times]
+
+
+def host_register(buf: np.ndarray) -> None:
+    """rt_host_register: page-lock a host frame (e.g. the `pixels` array) so
+    frame downloads into it are direct DMA."""
+    _check(library().rt_host_register(_ptr(buf), buf.nbytes), "rt_host_register")
+
+
+def host_unregister(buf: np.ndarray) -> None:
+    _check(library().rt_host_unregister(_ptr(buf)), "rt_host_unregister")
 
 
 class RayTracer:

@@ -2038,6 +2038,18 @@ int rt_render_device(rt_ctx* ctx, const rt_scene* device_scene, const float ray_
                   out_format, path, device_out, st, nullptr);
 }
 
+int rt_host_register(void* host_ptr, int64_t bytes) {
+    if (!host_ptr || bytes <= 0) return RT_ERR_INVALID_ARG;
+    HIP_TRY(hipHostRegister(host_ptr, (size_t)bytes, hipHostRegisterPortable));
+    return RT_OK;
+}
+
+int rt_host_unregister(void* host_ptr) {
+    if (!host_ptr) return RT_ERR_INVALID_ARG;
+    HIP_TRY(hipHostUnregister(host_ptr));
+    return RT_OK;
+}
+
 int rt_shared_alloc(rt_ctx* ctx, int64_t bytes, void** device_ptr, rt_ipc_handle* handle) {
     if (!ctx || bytes <= 0 || !device_ptr || !handle) return RT_ERR_INVALID_ARG;
     static_assert(sizeof(hipIpcMemHandle_t) == sizeof(rt_ipc_handle), "IPC handle size");

@@ -143,6 +143,7 @@ def test_bench_rehearsal_assemblies(world, tmp_path):
         assert line["assembly"][how]["frame_check"] == "bit-exact", line["assembly"]
         assert line["texture_rgba8"][how]["frame_check"] == "bit-exact"
         assert line["config4"][how]["frame_check"] == "bit-exact"
+    assert line["host_frame"]["frame_check"] == "bit-exact", line["host_frame"]
     assert line["value"] == pytest.approx(1024 * 512 / (line["ms_per_step"] * 1e-3) / 1e6,
                                           rel=2e-3)
 
@@ -191,3 +192,18 @@ def test_coarse_depth_cull_exact(pkg, rt, oracle, case):
     if fmt == "rgba8":
         want = oracle.pack_rgba8(want)
     assert np.array_equal(on, want)
+
+
+def test_render_into_registered_host_frame(pkg, rt):
+    """rt_host_register: rt_render's download into a page-locked host frame
+    (the app's `pixels` vector) gives the same frame, for bands too."""
+    g_scene = pkg.Scene.synthetic(333, 200, 40, 10, seed=21, k=1.2)
+    want, _ = rt.render(g_scene, 333, 200)
+    buf = np.zeros((200, 333, 4), np.int32)
+    pkg.host_register(buf)
+    try:
+        rt.render(g_scene, 333, 200, rows=(0, 77), out=buf[:77])
+        rt.render(g_scene, 333, 200, rows=(77, 200), out=buf[77:])
+    finally:
+        pkg.host_unregister(buf)
+    assert np.array_equal(buf, want)
