@@ -870,6 +870,14 @@ static_assert(kTiles <= 16 && kTmWords <= 4, "tile words");
 #endif
 constexpr int kRound = RT_C3_ROUND;
 static_assert(kTmWords == 1, "coarse depth cull: one tile word per candidate");
+#ifndef RT_COARSE_WAVES
+#define RT_COARSE_WAVES 6  // amdgpu_waves_per_eu floor for coarse3_kernel (0 = none): 80 VGPRs, 6 waves/SIMD (86 and 5 without; config 3 -0.4 us, config 5 dense -1.3%)
+#endif
+#if RT_COARSE_WAVES > 0
+#define RT_COARSE_ATTR __attribute__((amdgpu_waves_per_eu(RT_COARSE_WAVES)))
+#else
+#define RT_COARSE_ATTR
+#endif
 
 // Coarse depth cull (`cull`): an upper bound on every pixel's final closest
 // per wave tile, from the spheres that provably hit the WHOLE tile.  The
@@ -933,7 +941,7 @@ __device__ __forceinline__ unsigned tile_low_key(const SphRec& r, int tx, int ty
     return t == t ? order_key(t) : 0u;
 }
 
-__global__ void __launch_bounds__(64) coarse3_kernel(
+__global__ void __launch_bounds__(64) RT_COARSE_ATTR coarse3_kernel(
     const int4* __restrict__ boxes, const Cls* __restrict__ cls,
     const SphRec* __restrict__ sph, int n_prims, int n_tri,
     int n_cx, const unsigned long long* __restrict__ row_masks,
