@@ -379,14 +379,6 @@ __device__ __forceinline__ int4v shade(float closest, float4 colour) {
                  cvt_i32(scalar * colour.z), 255};
 }
 
-// Hot-path shade of a hit pixel (closest < 300000 always holds here).
-__device__ __forceinline__ int4v shade_hit(float closest, float4 colour) {
-    const float normalised = div180(closest - 0.0f);
-    const float scalar = 255.0f - (normalised * 255.0f);
-    return int4v{cvt_i32_fast(scalar * colour.x), cvt_i32_fast(scalar * colour.y),
-                 cvt_i32_fast(scalar * colour.z), 255};
-}
-
 __device__ __forceinline__ unsigned pack_rgba8(int4v p) {
     return (unsigned)(unsigned char)p.x | ((unsigned)(unsigned char)p.y << 8) |
            ((unsigned)(unsigned char)p.z << 16) | 0xFF000000u;
@@ -765,7 +757,9 @@ __device__ __forceinline__ void shade_pixels(const float4* __restrict__ colours,
         bool big = false;
 #pragma unroll
         for (int j = 0; j < kRowsPerLane; ++j) {
-            const float normalised = div180(hit[j] >= 0 ? closest[j] : 1.0f);
+            // a lane without a hit shades kFar (discarded below): on div180's
+            // fast path like every hit
+            const float normalised = div180(closest[j]);
             const float scalar = 255.0f - (normalised * 255.0f);
             f[j][0] = scalar * col[j].x;
             f[j][1] = scalar * col[j].y;
@@ -794,18 +788,43 @@ __device__ __forceinline__ void shade_pixels(const float4* __restrict__ colours,
     }
 #pragma unroll
     for (int j = 0; j < kRowsPerLane; ++j) pix[j] = int4v{0, 0, 0, 255};
-    if (any_hit) {
-        float4 col[kRowsPerLane];
+    if (!any_hit) return;
+    float4 col[kRowsPerLane];
 #pragma unroll
-        for (int j = 0; j < kRowsPerLane; ++j)  // kMode 4: no gather (diagnostics)
-            col[j] = kMode == 4 ? make_float4(1.0f, 0.5f, 0.25f, 255.0f)
-                                : colours[hit[j] >= 0 ? hit[j] : 0];
+    for (int j = 0; j < kRowsPerLane; ++j)  // kMode 4: no gather (diagnostics)
+        col[j] = kMode == 4 ? make_float4(1.0f, 0.5f, 0.25f, 255.0f)
+                            : colours[hit[j] >= 0 ? hit[j] : 0];
+    // x86's (int) and v_cvt_i32_f32 agree except on NaN (INT32_MIN vs 0) and
+    // f >= 2^31 (INT32_MIN vs INT32_MAX): one wave-uniform test picks the
+    // raw converts, the per-channel fix-ups (cvt_i32_fast) run only when some
+    // lane needs them.  Lanes without a hit shade kFar (discarded): on
+    // div180's fast path like every hit.
+    float f[kRowsPerLane][3];
+    bool fix = false;
+#pragma unroll
+    for (int j = 0; j < kRowsPerLane; ++j) {
+        const float normalised = div180(closest[j]);
+        const float scalar = 255.0f - (normalised * 255.0f);
+        f[j][0] = scalar * col[j].x;
+        f[j][1] = scalar * col[j].y;
+        f[j][2] = scalar * col[j].z;
+        fix |= !(fmaxf(fmaxf(f[j][0], f[j][1]), f[j][2]) < 2147483648.0f) |
+               __builtin_isunordered(f[j][0], f[j][1]) | __builtin_isunordered(f[j][2], f[j][2]);
+    }
+    if (__ballot(fix)) {
 #pragma unroll
         for (int j = 0; j < kRowsPerLane; ++j) {
-            // lanes without a hit shade a dummy 1.0 (discarded) so that div180
-            // stays on its fast path
-            const int4v c = shade_hit(hit[j] >= 0 ? closest[j] : 1.0f, col[j]);
-            if (hit[j] >= 0) pix[j] = c;
+            const int4v c{cvt_i32_fast(f[j][0]), cvt_i32_fast(f[j][1]), cvt_i32_fast(f[j][2]), 255};
+            pix[j] = hit[j] >= 0 ? c : pix[j];
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < kRowsPerLane; ++j) {
+            int c[3];
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+                asm volatile("v_cvt_i32_f32 %0, %1" : "=v"(c[k]) : "v"(f[j][k]));
+            pix[j] = hit[j] >= 0 ? int4v{c[0], c[1], c[2], 255} : pix[j];
         }
     }
 }
