@@ -58,8 +58,8 @@ CONFIG4 = dict(width=8192, height=8192, spheres=192, cubes=64, seed=4)
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--width", type=int, default=4096)
     ap.add_argument("--height", type=int, default=4096, help="frame rows (all ranks together)")
     ap.add_argument("--spheres", type=int, default=256)

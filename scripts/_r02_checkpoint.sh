@@ -1,0 +1,14 @@
+set -u
+cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out; export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
+TAG=${TAG:-r02cp}
+timeout -k 10 240 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1
+rc=$?; echo "smoke rc=$rc"; tail -1 gpurun_out/smoke_$TAG.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests -m gpu > gpurun_out/pytest_$TAG.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -2 gpurun_out/pytest_$TAG.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29514 bench.py --gpus 4 --rehearse --steps 10 --warmup 3 > gpurun_out/rehearse_${TAG}_4.json 2> gpurun_out/rehearse_${TAG}_4.err
+rc=$?; echo "rehearse4 rc=$rc"; [ $rc -ne 0 ] && { tail -20 gpurun_out/rehearse_${TAG}_4.err; exit $rc; }
+timeout -k 10 300 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err
+rc=$?; echo "bench rc=$rc"; cat gpurun_out/bench_$TAG.json; [ $rc -ne 0 ] && { tail -20 gpurun_out/bench_$TAG.err; exit $rc; }
+cd /tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG" -o run --output-format csv -- python "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline --no-host-path > "$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG.log" 2>&1
+rc=$?; echo "rocprof rc=$rc"; exit $rc
