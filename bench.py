@@ -394,13 +394,14 @@ class Assembly:
     """One frame (width x height, `fmt`) split into row bands over the ranks
     and assembled on rank 0 by `how` ("rccl_p2p" or "xgmi_peer_store")."""
 
-    def __init__(self, c: Ctx, pkg, rt, ds, width, height, fmt, how, path="auto"):
+    def __init__(self, c: Ctx, pkg, rt, ds, width, height, fmt, how, path="auto", bands=None):
         from opencl_ray_tracer_amd import rowbands
 
         self.c, self.rt, self.how, self.fmt = c, rt, how, fmt
         self.width, self.height = width, height
         self.rowbands = rowbands
-        self.rb, self.re = rowbands.band_rows(height, c.world, c.rank)
+        self.bands = bands or [rowbands.band_rows(height, c.world, r) for r in range(c.world)]
+        self.rb, self.re = self.bands[c.rank]
         self.root = c.rank == 0
         px_bytes = BYTES_PER_RAY[fmt]
         self.row_bytes = width * px_bytes
@@ -441,15 +442,16 @@ class Assembly:
         if self.how == "rccl_p2p":
             if c.backend == "nccl":
                 for q in self.rowbands.assemble_frame(self.frame, self.band, self.height, c.world,
-                                                      c.rank, async_op=True):
+                                                      c.rank, async_op=True, bands=self.bands):
                     q.wait()  # the stream waits; the host does not
             else:
                 c.sync()
                 hf = self.host_frame
-                self.rowbands.assemble_frame(hf, self.band.cpu(), self.height, c.world, c.rank)
+                self.rowbands.assemble_frame(hf, self.band.cpu(), self.height, c.world, c.rank,
+                                             bands=self.bands)
                 if self.root:  # the other ranks' rows, host -> device
                     for r in range(1, c.world):
-                        rb, re = self.rowbands.band_rows(self.height, c.world, r)
+                        rb, re = self.bands[r]
                         self.frame[rb:re].copy_(hf[rb:re])
         else:
             # every band landed in rank 0's frame once every rank's render
@@ -500,8 +502,8 @@ def _wrap_device(c: Ctx, ptr: int, rows, width, fmt):
     return torch.as_tensor(_Arr(), device=c.dev)
 
 
-def measure_assembly(args, c, pkg, rt, ds, width, height, fmt, how, split=False):
-    a = Assembly(c, pkg, rt, ds, width, height, fmt, how)
+def measure_assembly(args, c, pkg, rt, ds, width, height, fmt, how, split=False, bands=None):
+    a = Assembly(c, pkg, rt, ds, width, height, fmt, how, bands=bands)
     if a.error:
         a.close()  # frees what the root allocated; a barrier on every rank
         return {"ms_per_step": None, "error": a.error}
@@ -509,9 +511,10 @@ def measure_assembly(args, c, pkg, rt, ds, width, height, fmt, how, split=False)
         a.step()
     c.sync()
     ms = c.timed(a.step, args.steps)
+    rb0, re0 = a.bands[0]
     res = {"ms_per_step": round(ms, 4),
            "mrays": round(mrays_per_s(width * height, ms), 1),
-           "bytes_to_root": bytes_to_root(width, height, c.world, fmt)}
+           "bytes_to_root": BYTES_PER_RAY[fmt] * width * (height - (re0 - rb0))}
     if split:
         render_ms = c.timed(a.render_only, args.steps)
         # rccl_p2p: the local render; xgmi_peer_store: the render whose
@@ -523,8 +526,53 @@ def measure_assembly(args, c, pkg, rt, ds, width, height, fmt, how, split=False)
             res["assemble_ms"] = round(asm_ms, 4)
             res["assemble_gbs_into_root"] = round(res["bytes_to_root"] / (asm_ms * 1e-3) / 1e9, 1)
     res["frame_check"] = a.check(ds)
+    res["rows_per_rank"] = [re - rb for rb, re in a.bands]
     a.close()
     return res
+
+
+def calibrate_peer_store(args, c, pkg, rt, ds, width, height, fmt):
+    """Each rank's cost model t(n) = a + s n for rendering n rows into rank
+    0's shared frame (xGMI stores; rank 0's own stores are local), from two
+    band sizes rendered by all ranks at once.  Returns [(a_r, s_r)] in
+    seconds, rows, identical on every rank."""
+    from opencl_ray_tracer_amd import rowbands
+
+    row_bytes = width * BYTES_PER_RAY[fmt]
+    shared = rowbands.SharedFrame(rt, row_bytes * height, row_bytes, c.rank,
+                                  handle_device=c.coll_dev)
+    try:
+        if not shared.ok:
+            return None
+        times = []
+        sizes = [max(16, height // c.world), max(16, height // (2 * c.world))]
+        for n in sizes:
+            rb = c.rank * n
+            step = rt.bind_render_device(ds, width, height, (rb, rb + n), shared.ptr_of_row(rb),
+                                         fmt=fmt, stream=c.stream.cuda_stream)
+            for _ in range(args.warmup):
+                step()
+            c.sync()
+            c.barrier()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                step()
+            c.sync()
+            times.append((time.perf_counter() - t0) / args.steps)
+            c.barrier()
+        (n1, t1), (n2, t2) = zip(sizes, times)
+        slope = (t1 - t2) / (n1 - n2)
+        if not slope > 0.0:  # noise: the larger band alone, no fixed cost
+            slope, fixed = t1 / n1, 0.0
+        else:
+            fixed = max(0.0, t1 - slope * n1)
+        mine = c.torch.tensor([fixed, slope], dtype=c.torch.float64, device=c.coll_dev)
+        every = [c.torch.empty_like(mine) for _ in range(c.world)]
+        c.dist.all_gather(every, mine)
+        return [(float(e[0]), float(e[1])) for e in every]
+    finally:
+        c.sync()
+        shared.close()
 
 
 def measure_host_frame(args, c: Ctx, pkg, rt, scene, w, h, fmt="i32x4"):
@@ -610,6 +658,17 @@ def run_multi(args, c: Ctx, pkg):
 
     assemblies = {how: measure_assembly(args, c, pkg, rt, ds, w, h, args.format, how, split=True)
                   for how in ("rccl_p2p", "xgmi_peer_store")}
+    # The equal split makes every other rank wait on its xGMI link while
+    # rank 0's own rows need no transfer: size the bands by each rank's
+    # measured cost (render + stores into rank 0's frame) so that all ranks
+    # finish together (rowbands.balanced_bands).  Same frame, same end point.
+    costs = calibrate_peer_store(args, c, pkg, rt, ds, w, h, args.format)
+    if costs is not None:
+        bal = rowbands.balanced_bands(h, costs)
+        assemblies["xgmi_peer_store_balanced"] = measure_assembly(
+            args, c, pkg, rt, ds, w, h, args.format, "xgmi_peer_store", split=True, bands=bal)
+        assemblies["xgmi_peer_store_balanced"]["cost_model_us"] = [
+            {"fixed": round(a * 1e6, 2), "per_row": round(s * 1e6, 4)} for a, s in costs]
     best, entry = pick_value(assemblies)
     ms = entry["ms_per_step"]
 

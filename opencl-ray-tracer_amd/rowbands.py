@@ -27,6 +27,36 @@ def band_rows(height: int, world: int, rank: int) -> Tuple[int, int]:
     return rank * height // world, (rank + 1) * height // world
 
 
+def balanced_bands(height: int, costs) -> List[Tuple[int, int]]:
+    """Contiguous row bands, in rank order, sized so that every rank
+    finishes together under its own cost model t_r(n) = a_r + s_r * n
+    (fixed cost a_r, cost per row s_r): the water-filling solution of
+    min max_r t_r(n_r) subject to sum_r n_r = height, n_r >= 0.  Ranks whose
+    fixed cost alone exceeds the common finish time get no rows.  Rounding
+    leftovers go to rank 0."""
+    n = len(costs)
+    if n == 0 or height <= 0:
+        raise ValueError("bad band request")
+    a = [max(0.0, float(c[0])) for c in costs]
+    s = [float(c[1]) for c in costs]
+    if any(not (x > 0.0) for x in s):
+        raise ValueError("every rank needs a positive cost per row")
+    active = set(range(n))
+    while True:
+        t = (height + sum(a[r] / s[r] for r in active)) / sum(1.0 / s[r] for r in active)
+        drop = {r for r in active if t - a[r] < 0.0}
+        if not drop:
+            break
+        active -= drop
+    rows = [int((t - a[r]) / s[r] + 1e-6) if r in active else 0 for r in range(n)]
+    rows[0] += height - sum(rows)
+    bands, at = [], 0
+    for k in rows:
+        bands.append((at, at + k))
+        at += k
+    return bands
+
+
 def broadcast_scene(arrays: Optional[Dict[str, "np.ndarray"]], root: int, device,
                     group=None) -> Dict[str, "torch.Tensor"]:
     """Broadcast the packed scene arrays from `root` (None elsewhere) and
@@ -86,7 +116,8 @@ def gather_frame(band: "torch.Tensor", height: int, world: int, rank: int, root:
 
 
 def assemble_frame(frame: Optional["torch.Tensor"], band: "torch.Tensor", height: int,
-                   world: int, rank: int, root: int = 0, group=None, async_op: bool = False):
+                   world: int, rank: int, root: int = 0, group=None, async_op: bool = False,
+                   bands: Optional[List[Tuple[int, int]]] = None):
     """Assemble the frame on `root` by point-to-point transfers straight
     into the root's frame rows (RCCL P2P over xGMI with backend "nccl").
 
@@ -96,13 +127,14 @@ def assemble_frame(frame: Optional["torch.Tensor"], band: "torch.Tensor", height
     padding, staging list or concatenation on the root (unlike
     gather_frame).  Empty bands (height < world) send nothing.  With
     async_op the requests are returned (wait() orders the caller's stream
-    after them, without a host sync)."""
+    after them, without a host sync).  `bands`: each rank's (row_begin,
+    row_end) when not band_rows' equal split (e.g. balanced_bands)."""
     import torch.distributed as dist
 
     ops = []
     if rank == root:
         for r in range(world):
-            rb, re = band_rows(height, world, r)
+            rb, re = bands[r] if bands is not None else band_rows(height, world, r)
             if r != root and re > rb:
                 ops.append(dist.P2POp(dist.irecv, frame[rb:re], r, group))
     elif band.shape[0]:

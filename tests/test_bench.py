@@ -157,3 +157,27 @@ def test_render_distributed_more_ranks_than_rows(tmp_path):
     out = tmp_path / "frame.npy"
     mp.spawn(_empty_band_worker, args=(3, _free_port(), str(out)), nprocs=3, join=True)
     assert np.array_equal(np.load(out), np.array([[0] * 5, [1] * 5]))
+
+
+def test_balanced_bands():
+    import __graft_entry__
+    __graft_entry__.load_package()
+    from opencl_ray_tracer_amd.rowbands import balanced_bands
+
+    # equal costs: equal bands
+    b = balanced_bands(4096, [(1e-5, 1e-8)] * 4)
+    assert [e - s for s, e in b] == [1024] * 4
+    # rank 0 without a link costs 1/20 per row: it takes most rows, and every
+    # rank's modelled time is (nearly) equal
+    costs = [(1e-5, 1e-8)] + [(1e-5, 2e-7)] * 7
+    b = balanced_bands(4096, costs)
+    assert b[0][0] == 0 and b[-1][1] == 4096
+    assert all(x[1] == y[0] for x, y in zip(b, b[1:]))
+    rows = [e - s for s, e in b]
+    t = [a + s * n for (a, s), n in zip(costs, rows)]
+    assert rows[0] > 3000 and max(t) - min(t) <= 2 * max(s for _, s in costs) + 1e-12
+    # a rank whose fixed cost alone exceeds the finish time gets no rows
+    b = balanced_bands(100, [(0.0, 1e-6), (1.0, 1e-6)])
+    assert [e - s for s, e in b] == [100, 0]
+    with pytest.raises(ValueError):
+        balanced_bands(10, [(0.0, 0.0)])

@@ -144,6 +144,8 @@ def test_bench_rehearsal_assemblies(world, tmp_path):
         assert line["texture_rgba8"][how]["frame_check"] == "bit-exact"
         assert line["config4"][how]["frame_check"] == "bit-exact"
     assert line["host_frame"]["frame_check"] == "bit-exact", line["host_frame"]
+    bal = line["assembly"]["xgmi_peer_store_balanced"]
+    assert bal["frame_check"] == "bit-exact" and sum(bal["rows_per_rank"]) == 512, bal
     assert line["value"] == pytest.approx(1024 * 512 / (line["ms_per_step"] * 1e-3) / 1e6,
                                           rel=2e-3)
 
