@@ -647,6 +647,28 @@ def device_scene_from(c: Ctx, scene):
     return t, ds
 
 
+def measure_assemblies(args, c, pkg, rt, ds, w, h, fmt, split=False):
+    """The frame assembled on rank 0 three ways: equal bands by RCCL
+    point-to-point, equal bands by xGMI peer stores, and cost-balanced bands
+    by xGMI peer stores.  The equal split makes every other rank wait on its
+    link while rank 0's own rows need no transfer, so the balanced split
+    sizes the bands by each rank's measured cost (render + stores into rank
+    0's frame) for all ranks to finish together (rowbands.balanced_bands).
+    Same frame, same end point, each checked bit-exactly."""
+    from opencl_ray_tracer_amd import rowbands
+
+    res = {how: measure_assembly(args, c, pkg, rt, ds, w, h, fmt, how, split=split)
+           for how in ("rccl_p2p", "xgmi_peer_store")}
+    costs = calibrate_peer_store(args, c, pkg, rt, ds, w, h, fmt)
+    if costs is not None:
+        bal = rowbands.balanced_bands(h, costs)
+        res["xgmi_peer_store_balanced"] = measure_assembly(
+            args, c, pkg, rt, ds, w, h, fmt, "xgmi_peer_store", split=split, bands=bal)
+        res["xgmi_peer_store_balanced"]["cost_model_us"] = [
+            {"fixed": round(a * 1e6, 2), "per_row": round(s * 1e6, 4)} for a, s in costs]
+    return res
+
+
 def run_multi(args, c: Ctx, pkg):
     from opencl_ray_tracer_amd import rowbands
 
@@ -656,19 +678,7 @@ def run_multi(args, c: Ctx, pkg):
     rt = pkg.RayTracer(c.gpu)
     rb, re = rowbands.band_rows(h, c.world, c.rank)
 
-    assemblies = {how: measure_assembly(args, c, pkg, rt, ds, w, h, args.format, how, split=True)
-                  for how in ("rccl_p2p", "xgmi_peer_store")}
-    # The equal split makes every other rank wait on its xGMI link while
-    # rank 0's own rows need no transfer: size the bands by each rank's
-    # measured cost (render + stores into rank 0's frame) so that all ranks
-    # finish together (rowbands.balanced_bands).  Same frame, same end point.
-    costs = calibrate_peer_store(args, c, pkg, rt, ds, w, h, args.format)
-    if costs is not None:
-        bal = rowbands.balanced_bands(h, costs)
-        assemblies["xgmi_peer_store_balanced"] = measure_assembly(
-            args, c, pkg, rt, ds, w, h, args.format, "xgmi_peer_store", split=True, bands=bal)
-        assemblies["xgmi_peer_store_balanced"]["cost_model_us"] = [
-            {"fixed": round(a * 1e6, 2), "per_row": round(s * 1e6, 4)} for a, s in costs]
+    assemblies = measure_assemblies(args, c, pkg, rt, ds, w, h, args.format, split=True)
     best, entry = pick_value(assemblies)
     ms = entry["ms_per_step"]
 
@@ -693,8 +703,7 @@ def run_multi(args, c: Ctx, pkg):
     extras = {}
     if not args.no_extras:
         # the Texture (RGBA8, MainState.cpp:1023-1037) assembled the same way
-        extras["texture_rgba8"] = {how: measure_assembly(args, c, pkg, rt, ds, w, h, "rgba8", how)
-                                   for how in ("rccl_p2p", "xgmi_peer_store")}
+        extras["texture_rgba8"] = measure_assemblies(args, c, pkg, rt, ds, w, h, "rgba8")
         # BASELINE config 4: 8192^2, 192 + 64, row-tiled with the assembly
         c4 = CONFIG4
         k4 = c4["width"] / 640.0
@@ -704,8 +713,7 @@ def run_multi(args, c: Ctx, pkg):
             "workload": f"config4: {c4['width']}x{c4['height']} frame, {c4['spheres']} spheres + "
                         f"{c4['cubes']} cubes, dense k={k4:.1f}, seed {c4['seed']}, "
                         f"{c.world} row bands (BASELINE names 8 GPUs)",
-            **{how: measure_assembly(args, c, pkg, rt, ds4, c4["width"], c4["height"], "i32x4",
-                                     how) for how in ("rccl_p2p", "xgmi_peer_store")}}
+            **measure_assemblies(args, c, pkg, rt, ds4, c4["width"], c4["height"], "i32x4")}
         del ds4
         # weak scaling (secondary): a 4096 x 4096N frame with N x (256 + 64)
         # primitives of the same density, rank r renders rows [4096 r, 4096 (r+1))
