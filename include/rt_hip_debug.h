@@ -67,6 +67,14 @@ int rt_debug_set_small_path(rt_ctx* ctx, int enable);
  * `enable` sphere candidates (1 = every bin, 0 = off: every candidate the tile
  * classifier keeps stays; negative = the build's default; A/B and tests). */
 int rt_debug_set_coarse_cull(rt_ctx* ctx, int enable);
+/* Wave-tile build used by the binned path: 0 = by frame size (64x4 tiles
+ * for frames of >= 1 GiB, else 16x16), 1 = 16x16, 2 = 64x4. */
+int rt_debug_set_tile_variant(rt_ctx* ctx, int variant);
+/* The 64x4 build's triangle prep and tile shape (host culling tests). */
+int rt_debug_triangle_box_wide(const float v0[3], const float v1[3], const float v2[3],
+                               const float dir[4], int32_t width, int32_t row_begin,
+                               int32_t row_end, int32_t box_out[4], float cls_out[8]);
+int rt_debug_tile_shape_wide(int32_t* w, int32_t* h);
 
 /* Host evaluation of the device's restatement of glibc 2.35 sinf / cosf
  * (the same __host__ __device__ code rt_cube_build_device runs), for the

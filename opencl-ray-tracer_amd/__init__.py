@@ -152,6 +152,8 @@ def library() -> ctypes.CDLL:
         "rt_debug_set_bin_masks": (ctypes.c_int, [vp, ctypes.c_int]),
         "rt_debug_set_small_path": (ctypes.c_int, [vp, ctypes.c_int]),
         "rt_debug_set_coarse_cull": (ctypes.c_int, [vp, ctypes.c_int]),
+        "rt_debug_set_tile_variant": (ctypes.c_int, [vp, ctypes.c_int]),
+        "rt_debug_triangle_box_wide": (ctypes.c_int, [vp, vp, vp, vp, i32, i32, i32, vp, vp]),
         "rt_cube_build_device": (ctypes.c_int, [vp, vp, vp, i32, vp, vp, vp]),
         "rt_scene_synthetic_device": (ctypes.c_int, [vp, i32, i32, i32, i32, ctypes.c_uint64,
                                                      f32, vp, vp, vp, vp, vp, vp]),
@@ -504,6 +506,12 @@ class RayTracer:
         _check(library().rt_debug_set_small_path(self._ctx, int(enable)),
                "rt_debug_set_small_path")
 
+    def set_tile_variant(self, variant: int) -> None:
+        """Diagnostics: the binned path's wave-tile build (0 = by frame size,
+        1 = 16x16, 2 = 64x4)."""
+        _check(library().rt_debug_set_tile_variant(self._ctx, int(variant)),
+               "rt_debug_set_tile_variant")
+
     def set_coarse_cull(self, min_candidates) -> None:
         """Diagnostics: the coarse kernel's depth cull of sphere candidates,
         in bins with at least `min_candidates` candidates (True = every bin,
@@ -566,6 +574,18 @@ def debug_triangle_prep(v0, v1, v2, ray_dir, width, row_begin, row_end):
     cls = np.zeros(8, np.float32)
     ok = library().rt_debug_triangle_box(_ptr(a[0]), _ptr(a[1]), _ptr(a[2]), _ptr(d), width,
                                          row_begin, row_end, _ptr(box), _ptr(cls))
+    return bool(ok), box, cls
+
+
+def debug_triangle_prep_wide(v0, v1, v2, ray_dir, width, row_begin, row_end):
+    """debug_triangle_prep of the 64x4-tile build (its classifier margin
+    covers 64-pixel tile spans)."""
+    a = [np.ascontiguousarray(v, np.float32)[:3].copy() for v in (v0, v1, v2)]
+    d = np.ascontiguousarray(ray_dir, np.float32)
+    box = np.zeros(4, np.int32)
+    cls = np.zeros(8, np.float32)
+    ok = library().rt_debug_triangle_box_wide(_ptr(a[0]), _ptr(a[1]), _ptr(a[2]), _ptr(d), width,
+                                              row_begin, row_end, _ptr(box), _ptr(cls))
     return bool(ok), box, cls
 
 

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Build compile-time variants of librt_hip.so for A/B timing
 # (scripts/bench_variants.py).  Usage: scripts/variants.sh name:"-DFLAG=.." ...
+# (tile widths: -DRT_TILE_NARROW=.. / -DRT_TILE_WIDE=.., not RT_TILE_W)
 set -e
 R="$(cd "$(dirname "$0")/.." && pwd)"
 C="$R/opencl-ray-tracer_amd/csrc"; V="$R/opencl-ray-tracer_amd/variants"

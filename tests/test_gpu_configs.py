@@ -209,3 +209,42 @@ def test_render_into_registered_host_frame(pkg, rt):
     finally:
         pkg.host_unregister(buf)
     assert np.array_equal(buf, want)
+
+
+@pytest.mark.parametrize("case", ["golden", "dense", "rgba8", "bands", "culled", "edges"])
+def test_wide_tile_build_exact(pkg, rt, oracle, case):
+    """The 64x4-tile build (auto-selected for frames of >= 1 GiB) forced on
+    small frames: bit-exact against the oracle / golden frames and against
+    the 16x16 build, on awkward sizes, bands, both formats and the coarse
+    depth cull."""
+    from conftest import golden_scene, load_golden
+
+    try:
+        rt.set_tile_variant(2)
+        if case == "golden":
+            for name in ("scene1_640x480", "scene3_640x480", "config2_1920x1080"):
+                g = load_golden(name)
+                got, t = rt.render(golden_scene(pkg, g), int(g["width"]), int(g["height"]))
+                assert np.array_equal(got, g["frame"]), name
+            return
+        w, h = (333, 257) if case != "edges" else (130, 67)
+        if case == "culled":
+            scene = pkg.Scene.synthetic(640, 480, 1200, 0, seed=5, k=4.0)
+            w, h = 640, 480
+        elif case == "edges":
+            scene = pkg.Scene.synthetic(w, h, 30, 12, seed=8, k=0.4)
+        else:
+            scene = pkg.Scene.synthetic(w, h, 60, 16, seed=104, k=w / 640 * 2)
+        fmt = "rgba8" if case == "rgba8" else "i32x4"
+        rows = (37, 201) if case == "bands" else (0, h)
+        wide, t = rt.render(scene, w, h, rows=rows, fmt=fmt)
+        assert t.path == "binned"
+        rt.set_tile_variant(1)
+        narrow, _ = rt.render(scene, w, h, rows=rows, fmt=fmt)
+        assert np.array_equal(wide, narrow)
+        want = oracle.trace(scene, w, h, rows=rows, threads=THREADS)
+        if fmt == "rgba8":
+            want = oracle.pack_rgba8(want)
+        assert np.array_equal(wide, want)
+    finally:
+        rt.set_tile_variant(0)

@@ -150,16 +150,32 @@ def classify_pixels(cls, xs, ys):
     return out, inside
 
 
+def wide_tile_shape(pkg):
+    w, h = ctypes.c_int32(), ctypes.c_int32()
+    assert pkg.library().rt_debug_tile_shape_wide(ctypes.byref(w), ctypes.byref(h)) == 0
+    return w.value, h.value
+
+
+@pytest.mark.parametrize("build", ["narrow", "wide"])
 @pytest.mark.parametrize("band", [(0, 160), (37, 121)])
-def test_triangle_box_and_tile_classifier_are_conservative(pkg, oracle, band):
+def test_triangle_box_and_tile_classifier_are_conservative(pkg, oracle, band, build):
+    """Both wave-tile builds (16x16 and 64x4 tiles; each has its own
+    classifier margin for its tile span)."""
     w, h = 176, 160
     rb, re = band
-    tw, th = tile_shape(pkg)
-    shapes = classified_shapes(pkg)
+    if build == "narrow":
+        tw, th = tile_shape(pkg)
+        shapes = classified_shapes(pkg)
+        prep = pkg.debug_triangle_prep
+    else:
+        tw, th = wide_tile_shape(pkg)
+        assert (tw, th) == (64, 4)
+        shapes = [(tw, th)]
+        prep = pkg.debug_triangle_prep_wide
     rng = np.random.default_rng(7 + rb)
     n_inside_tiles = n_skip_tiles = 0
     for v in random_triangles(rng, w, h, 150):
-        ok, box, cls = pkg.debug_triangle_prep(v[0], v[1], v[2], RAY_DIR, w, rb, re)
+        ok, box, cls = prep(v[0], v[1], v[2], RAY_DIR, w, rb, re)
         hits = oracle.tri_grid(v[0], v[1], v[2], RAY_DIR, 0, rb, w, re - rb)
         if not ok:
             assert not hits.any()
