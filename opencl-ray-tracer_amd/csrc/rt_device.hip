@@ -22,6 +22,11 @@
 // Plus `generic`, a brute-force per-pixel kernel for arbitrary ray origins
 // and directions (the reference's kernel arguments 8-9 in full generality).
 //
+// The kernels and their host launch() are in rt_trace.inc, compiled here
+// twice: 16x16 wave tiles (namespace tile16) and 64x4 tiles (tile64, frames
+// of >= 1 GiB, whose stores drain faster from 1-KiB rows).
+// This file holds the context, the dispatcher and the C ABI.
+//
 // Build: -ffp-contract=off (and the pragma below): every operation rounds
 // once, as x86-64 SSE does in the reference's CPU build.
 #include <hip/hip_ext.h>
