@@ -96,7 +96,9 @@ const char* rt_error_string(int status);
  *   ray_dir       float4, the reference passes (0,0,-1,-1) (MainState.cpp:37-39)
  *   ray_origins   NULL for the reference's implicit (x, y, 0, 1) grid
  *                 (MainState.cpp:44-50), else float4[width*height] (full
- *                 frame; only rows [row_begin, row_end) are uploaded)
+ *                 frame; only rows [row_begin, row_end) are uploaded, and
+ *                 origins that are bit for bit that grid are recognised on
+ *                 the device and keep the binned path)
  *   host_out      int32[4*width*rows] (I32X4) or uint32[width*rows] (RGBA8)
  *   timing        may be NULL
  * Empty scenes are legal (all pixels (0,0,0,255)). */

@@ -192,6 +192,25 @@ __global__ void fp32_selftest_kernel(const float* in, int n, float* out_sqrt, fl
     out_div[i] = in[i] / 180.0f;
 }
 
+// Are the explicit ray origins of rows [row_begin, row_begin + n / width)
+// exactly the reference's implicit grid (x, y, 0, 1) (MainState.cpp:44-50)?
+// Bitwise comparison; any other value sets *flag (one atomic per wave).
+// `origins` starts at the band's first row.
+__global__ void __launch_bounds__(256) grid_check_kernel(const float4* __restrict__ origins,
+                                                         int width, int row_begin, int64_t n,
+                                                         unsigned* __restrict__ flag) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    bool off = false;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const float4 o = origins[i];
+        const int x = (int)(i % width), y = row_begin + (int)(i / width);
+        off |= __float_as_uint(o.x) != __float_as_uint((float)x) ||
+               __float_as_uint(o.y) != __float_as_uint((float)y) || __float_as_uint(o.z) != 0u ||
+               __float_as_uint(o.w) != __float_as_uint(1.0f);
+    }
+    if (__ballot(off) != 0ull && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
+}
+
 // Frames of at least this many bytes take the wide tiles (auto selection).
 constexpr int64_t kWideTileBytes = (int64_t)1 << 30;
 
@@ -247,7 +266,7 @@ int rt_init(int device_ordinal, rt_ctx** out_ctx) {
             return RT_ERR_HIP;
         }
     }
-    // [0] non-finite flag
+    // [0] non-finite flag, [1] explicit-origin grid check
     if (hipMalloc(&ctx->flag, 4 * sizeof(unsigned)) != hipSuccess ||
         hipMemset(ctx->flag, 0, 4 * sizeof(unsigned)) != hipSuccess) {
         rt_destroy(ctx);
@@ -315,6 +334,21 @@ int rt_render_path(rt_ctx* ctx, const rt_scene* scene, const float ray_dir[4],
         HIP_TRY(hipMemcpyAsync(ctx->origin_buf, ray_origins + (size_t)4 * width * row_begin, ob,
                                hipMemcpyHostToDevice, st));
         d_origins = static_cast<const float*>(ctx->origin_buf);
+        if (path != RT_PATH_GENERIC && binned_ok(ray_dir, nullptr)) {
+            // The reference always uploads its implicit (x, y, 0, 1) grid:
+            // check the origins on the device (one streaming read) and keep
+            // the binned path when they are exactly that grid.
+            unsigned off = 1u;
+            HIP_TRY(hipMemsetAsync(ctx->flag + 1, 0, sizeof(unsigned), st));
+            const int64_t blocks = std::min<int64_t>(((int64_t)px + 255) / 256, 4096);
+            grid_check_kernel<<<dim3((unsigned)blocks), dim3(256), 0, st>>>(
+                static_cast<const float4*>(ctx->origin_buf), width, row_begin, (int64_t)px,
+                ctx->flag + 1);
+            HIP_TRY(hipGetLastError());
+            HIP_TRY(hipMemcpyAsync(&off, ctx->flag + 1, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
+            if (off == 0u) d_origins = nullptr;
+        }
     }
     rt_scene dscene = *scene;
     dscene.sphere_origins = reinterpret_cast<const float*>(sb + o_so);

@@ -74,14 +74,29 @@ def test_row_bands_assemble(pkg, rt):
 
 
 def test_explicit_origins_match(pkg, rt):
-    """The reference uploads rayOrigins (MainState.cpp:44-50, :841-855);
-    passing them explicitly takes the generic kernel and must agree."""
+    """The reference uploads rayOrigins (MainState.cpp:44-50, :841-855):
+    passed explicitly they are recognised as the implicit grid on the device
+    and keep the binned path; any other origin value (one pixel off, a -0.0
+    z) takes the generic kernel.  Every frame equals the golden one where
+    the rays are the same."""
     g = load_golden("scene2_640x480")
+    scene = golden_scene(pkg, g)
     ys, xs = np.mgrid[0:480, 0:640]
     org = np.stack([xs, ys, np.zeros_like(xs), np.ones_like(xs)], -1).astype(np.float32)
-    frame, t = rt.render(golden_scene(pkg, g), 640, 480, ray_origins=org)
+    frame, t = rt.render(scene, 640, 480, ray_origins=org)
+    assert t.path == "binned"
+    assert np.array_equal(frame, g["frame"])
+    band, t = rt.render(scene, 640, 480, rows=(100, 333), ray_origins=org)
+    assert t.path == "binned" and np.array_equal(band, g["frame"][100:333])
+    negz = org.copy()
+    negz[5, 7, 2] = -0.0
+    frame, t = rt.render(scene, 640, 480, ray_origins=negz)
     assert t.path == "generic"
     assert np.array_equal(frame, g["frame"])
+    off = org.copy()
+    off[479, 639, 0] = 639.5
+    _, t = rt.render(scene, 640, 480, ray_origins=off)
+    assert t.path == "generic"
 
 
 @pytest.mark.parametrize("seed", [1, 2, 3])
@@ -480,8 +495,10 @@ def test_error_paths_on_device(pkg, rt):
     origins = np.zeros((h, w, 4), np.float32)
     origins[..., 0], origins[..., 1] = np.meshgrid(np.arange(w), np.arange(h))
     origins[..., 3] = 1.0
+    shifted = origins.copy()
+    shifted[..., 0] += 0.25  # not the implicit grid
     with pytest.raises(pkg.RtError) as e:
-        rt.render(scene, w, h, ray_origins=origins, path="binned")
+        rt.render(scene, w, h, ray_origins=shifted, path="binned")
     assert e.value.status == pkg.RT_ERR_UNSUPPORTED
     with pytest.raises(pkg.RtError) as e:
         rt.render(scene, w, h, ray_dir=np.float32([0.3, 0.0, -1.0, -1.0]), path="binned")
@@ -490,12 +507,14 @@ def test_error_paths_on_device(pkg, rt):
         with pytest.raises(pkg.RtError) as e:
             rt.render(scene, w, h, rows=rows)
         assert e.value.status == pkg.RT_ERR_INVALID_ARG
-    # explicit origins equal to the implicit grid take the generic path and
-    # give the same frame as the binned one
+    # explicit origins equal to the implicit grid (what the reference
+    # uploads, MainState.cpp:44-50) keep the binned path; forcing the
+    # generic kernel gives the same frame
     frame, t = rt.render(scene, w, h)
     same, t2 = rt.render(scene, w, h, ray_origins=origins)
-    assert (t.path, t2.path) == ("binned", "generic")
-    assert np.array_equal(frame, same)
+    gen, t3 = rt.render(scene, w, h, ray_origins=origins, path="generic")
+    assert (t.path, t2.path, t3.path) == ("binned", "binned", "generic")
+    assert np.array_equal(frame, same) and np.array_equal(frame, gen)
 
 
 def test_very_many_primitives(pkg, rt, oracle):
