@@ -67,6 +67,20 @@ int rt_debug_set_small_path(rt_ctx* ctx, int enable);
  * `enable` sphere candidates (1 = every bin, 0 = off: every candidate the tile
  * classifier keeps stays; negative = the build's default; A/B and tests). */
 int rt_debug_set_coarse_cull(rt_ctx* ctx, int enable);
+/* Triangles join the coarse depth cull in bins whose wave tiles keep at
+ * least this many candidates on average (0 = never, negative = the build's
+ * default). */
+int rt_debug_set_coarse_cull_tri(rt_ctx* ctx, int min_candidates);
+/* ... and only in frames whose primitive boxes, summed, cover the frame at
+ * least `frames` times (the trace is then bound by its tests rather than its
+ * stores; 0 = every frame, negative = the build's default). */
+int rt_debug_set_coarse_cull_overdraw(rt_ctx* ctx, int frames);
+/* The bounds tri_t_bounds gives the trace's computed fp64 t over pixels
+ * [xa, xb] x [ya, yb] (host evaluation; returns 0 without a bound). */
+int rt_debug_triangle_t_bounds(const float v0[3], const float v1[3], const float v2[3],
+                               const float dir[4], int32_t width, int32_t row_begin,
+                               int32_t row_end, int32_t xa, int32_t xb, int32_t ya, int32_t yb,
+                               double out[2]);
 /* Wave-tile build used by the binned path: 0 = by frame size (64x4 tiles
  * for frames of >= 1 GiB, else 16x16), 1 = 16x16, 2 = 64x4. */
 int rt_debug_set_tile_variant(rt_ctx* ctx, int variant);

@@ -153,6 +153,10 @@ def library() -> ctypes.CDLL:
         "rt_debug_set_small_path": (ctypes.c_int, [vp, ctypes.c_int]),
         "rt_debug_set_coarse_cull": (ctypes.c_int, [vp, ctypes.c_int]),
         "rt_debug_set_tile_variant": (ctypes.c_int, [vp, ctypes.c_int]),
+        "rt_debug_set_coarse_cull_tri": (ctypes.c_int, [vp, ctypes.c_int]),
+        "rt_debug_set_coarse_cull_overdraw": (ctypes.c_int, [vp, ctypes.c_int]),
+        "rt_debug_triangle_t_bounds": (ctypes.c_int, [vp, vp, vp, vp, i32, i32, i32, i32, i32,
+                                                      i32, i32, vp]),
         "rt_debug_triangle_box_wide": (ctypes.c_int, [vp, vp, vp, vp, i32, i32, i32, vp, vp]),
         "rt_cube_build_device": (ctypes.c_int, [vp, vp, vp, i32, vp, vp, vp]),
         "rt_scene_synthetic_device": (ctypes.c_int, [vp, i32, i32, i32, i32, ctypes.c_uint64,
@@ -506,6 +510,18 @@ class RayTracer:
         _check(library().rt_debug_set_small_path(self._ctx, int(enable)),
                "rt_debug_set_small_path")
 
+    def set_coarse_cull_tri(self, min_candidates: int) -> None:
+        """Diagnostics: triangles join the coarse depth cull in bins with at
+        least this many candidates (0 = never, negative = default)."""
+        _check(library().rt_debug_set_coarse_cull_tri(self._ctx, int(min_candidates)),
+               "rt_debug_set_coarse_cull_tri")
+
+    def set_coarse_cull_overdraw(self, frames: int) -> None:
+        """Diagnostics: ... and only in frames whose boxes cover the frame at
+        least this many times (0 = every frame, negative = default)."""
+        _check(library().rt_debug_set_coarse_cull_overdraw(self._ctx, int(frames)),
+               "rt_debug_set_coarse_cull_overdraw")
+
     def set_tile_variant(self, variant: int) -> None:
         """Diagnostics: the binned path's wave-tile build (0 = by frame size,
         1 = 16x16, 2 = 64x4)."""
@@ -587,6 +603,17 @@ def debug_triangle_prep_wide(v0, v1, v2, ray_dir, width, row_begin, row_end):
     ok = library().rt_debug_triangle_box_wide(_ptr(a[0]), _ptr(a[1]), _ptr(a[2]), _ptr(d), width,
                                               row_begin, row_end, _ptr(box), _ptr(cls))
     return bool(ok), box, cls
+
+
+def debug_triangle_t_bounds(v0, v1, v2, ray_dir, width, row_begin, row_end, xa, xb, ya, yb):
+    """Host evaluation of the coarse kernel's fp64 bounds of the trace's
+    computed t over pixels [xa, xb] x [ya, yb] (None without a bound)."""
+    a = [np.ascontiguousarray(v, np.float32)[:3].copy() for v in (v0, v1, v2)]
+    d = np.ascontiguousarray(ray_dir, np.float32)
+    out = np.zeros(2, np.float64)
+    ok = library().rt_debug_triangle_t_bounds(_ptr(a[0]), _ptr(a[1]), _ptr(a[2]), _ptr(d), width,
+                                              row_begin, row_end, xa, xb, ya, yb, _ptr(out))
+    return (float(out[0]), float(out[1])) if ok else None
 
 
 def debug_sphere_prep(origin, radius, ray_dir, width, row_begin, row_end):

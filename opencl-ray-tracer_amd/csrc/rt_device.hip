@@ -53,6 +53,14 @@
 #ifndef RT_COARSE_CULL
 #define RT_COARSE_CULL 10  // default of rt_debug_set_coarse_cull: bins with >= 10 sphere candidates
 #endif
+#ifndef RT_COARSE_CULL_TRI
+#define RT_COARSE_CULL_TRI 4  // default of rt_debug_set_coarse_cull_tri: triangles join the cull
+                              // in bins whose tiles keep >= this many candidates on average
+#endif
+#ifndef RT_COARSE_CULL_OVERDRAW
+#define RT_COARSE_CULL_OVERDRAW 5  // default of rt_debug_set_coarse_cull_overdraw: ... in frames
+                                   // whose primitive boxes cover the frame >= 5 times
+#endif
 
 // ===========================================================================
 // Host side
@@ -78,6 +86,11 @@ struct rt_ctx {
     // coarse depth cull of sphere candidates in bins with at least this many
     // candidates (0 = off)
     int coarse_cull = RT_COARSE_CULL;
+    // triangles join the depth cull in bins whose tiles keep at least this
+    // many candidates on average (0 = never)
+    int coarse_cull_tri = RT_COARSE_CULL_TRI;
+    // ... in frames whose boxes' summed area is at least this many frames
+    unsigned coarse_cull_overdraw = RT_COARSE_CULL_OVERDRAW;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     // profiling: per render, start/stop events of the prep, coarse and trace
     // kernels, attached to the kernels' own dispatch packets
@@ -266,7 +279,8 @@ int rt_init(int device_ordinal, rt_ctx** out_ctx) {
             return RT_ERR_HIP;
         }
     }
-    // [0] non-finite flag, [1] explicit-origin grid check
+    // [0] non-finite flag, [1] explicit-origin grid check, [2..3] the frame's
+    // box overdraw (generation-stamped, see prep_kernel)
     if (hipMalloc(&ctx->flag, 4 * sizeof(unsigned)) != hipSuccess ||
         hipMemset(ctx->flag, 0, 4 * sizeof(unsigned)) != hipSuccess) {
         rt_destroy(ctx);
@@ -622,6 +636,36 @@ int rt_debug_set_coarse_cull(rt_ctx* ctx, int enable) {
     if (!ctx) return RT_ERR_INVALID_ARG;
     ctx->coarse_cull = enable < 0 ? RT_COARSE_CULL : enable;  // < 0: the default
     return RT_OK;
+}
+
+int rt_debug_set_coarse_cull_tri(rt_ctx* ctx, int min_candidates) {
+    if (!ctx) return RT_ERR_INVALID_ARG;
+    ctx->coarse_cull_tri = min_candidates < 0 ? RT_COARSE_CULL_TRI : min_candidates;
+    return RT_OK;
+}
+
+int rt_debug_set_coarse_cull_overdraw(rt_ctx* ctx, int frames) {
+    if (!ctx) return RT_ERR_INVALID_ARG;
+    ctx->coarse_cull_overdraw = frames < 0 ? RT_COARSE_CULL_OVERDRAW : (unsigned)frames;
+    return RT_OK;
+}
+
+// tri_t_bounds of the 16x16 build's prep output (the TriDepth model), for
+// the host tests: fp64 bounds of the trace's computed t over pixels
+// [xa, xb] x [ya, yb].
+int rt_debug_triangle_t_bounds(const float v0[3], const float v1[3], const float v2[3],
+                               const float dir[4], int32_t width, int32_t row_begin,
+                               int32_t row_end, int32_t xa, int32_t xb, int32_t ya, int32_t yb,
+                               double out[2]) {
+    TriRec r{};
+    TriDepth d{0.0, 0.0, 0.0, INFINITY, 0.0, 0.0};
+    Box b{};
+    Cls k{};
+    bool bad = false;
+    if (!prep_triangle(v0, v1, v2, dir[0], dir[1], dir[2], width, row_begin, row_end, &r, &b, &k,
+                       &bad, &d))
+        return 0;
+    return tri_t_bounds(d, xa, xb, ya, yb, &out[0], &out[1]) ? 1 : 0;
 }
 
 int rt_debug_set_small_path(rt_ctx* ctx, int enable) {

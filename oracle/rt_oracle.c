@@ -635,6 +635,20 @@ void orc_tri_grid(const float v0[3], const float v1[3], const float v2[3], const
         }
 }
 
+/* The same grid with the reference's fp64 t of every hit pixel (NaN where
+ * the test misses), MainState.cpp:257-298. */
+void orc_tri_t_grid(const float v0[3], const float v1[3], const float v2[3], const float dir[4],
+                    int32_t x0, int32_t y0, int32_t w, int32_t h, double* ts) {
+    const double a[3] = {v0[0], v0[1], v0[2]}, b[3] = {v1[0], v1[1], v1[2]},
+                 c[3] = {v2[0], v2[1], v2[2]}, d[3] = {dir[0], dir[1], dir[2]};
+    for (int32_t j = 0; j < h; ++j)
+        for (int32_t i = 0; i < w; ++i) {
+            const double o[3] = {(double)(float)(x0 + i), (double)(float)(y0 + j), 0.0};
+            double t, u, v;
+            ts[(int64_t)j * w + i] = orc_intersect_tri(o, d, a, b, c, &t, &u, &v) ? t : NAN;
+        }
+}
+
 void orc_sphere_grid(const float centre[4], float radius, const float dir[4], int32_t x0,
                      int32_t y0, int32_t w, int32_t h, uint8_t* hits) {
     for (int32_t j = 0; j < h; ++j)

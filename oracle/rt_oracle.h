@@ -113,6 +113,8 @@ void orc_trace_cl32(int32_t width, int32_t height, const float ray_dir[4],
 void orc_tri_grid(const float v0[3], const float v1[3], const float v2[3],
                   const float dir[4], int32_t x0, int32_t y0, int32_t w, int32_t h,
                   uint8_t* hits);
+void orc_tri_t_grid(const float v0[3], const float v1[3], const float v2[3], const float dir[4],
+                    int32_t x0, int32_t y0, int32_t w, int32_t h, double* ts);
 void orc_sphere_grid(const float centre[4], float radius, const float dir[4],
                      int32_t x0, int32_t y0, int32_t w, int32_t h, uint8_t* hits);
 

@@ -29,13 +29,18 @@ CONFIGS = {
     "c5s": (16384, 16384, (0, 16384), 4096, 0, 5, 1.0),
     # rank 0's band of bench.py's 8-rank weak-scaling workload
     "band8": (4096, 32768, (0, 4096), 2048, 512, 3, 6.4),
+    # scenes of 4x and 16x config 3's object count at the same density
+    "c3x4": (4096, 4096, (0, 4096), 1024, 256, 3, 6.4),
+    "c3x16": (4096, 4096, (0, 4096), 4096, 1024, 3, 6.4),
+    "c3x64": (4096, 4096, (0, 4096), 16384, 4096, 3, 6.4),
 }
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--knob", default="coarse_cull",
-                    choices=("coarse_cull", "small_path", "bin_masks", "trace_mode"))
+                    choices=("coarse_cull", "coarse_cull_tri", "coarse_cull_overdraw", "small_path", "bin_masks",
+                             "trace_mode"))
     ap.add_argument("--values", default="0,1")
     ap.add_argument("--configs", default="c3,c5d,c5s,band8")
     ap.add_argument("--format", default="i32x4", choices=("i32x4", "rgba8"))
@@ -51,7 +56,9 @@ def main():
     dev = torch.device("cuda:0")
     stream = torch.cuda.Stream(dev)
     rt = pkg.RayTracer(0)
-    setter = {"coarse_cull": rt.set_coarse_cull, "small_path": rt.set_small_path,
+    setter = {"coarse_cull": rt.set_coarse_cull, "coarse_cull_tri": rt.set_coarse_cull_tri,
+              "coarse_cull_overdraw": rt.set_coarse_cull_overdraw,
+              "small_path": rt.set_small_path,
               "bin_masks": rt.set_bin_masks, "trace_mode": rt.set_trace_mode}[args.knob]
     values = [int(v) for v in args.values.split(",")]
     for cname in args.configs.split(","):

@@ -55,6 +55,7 @@ def _load() -> ctypes.CDLL:
         "orc_trace_cl32": (None, [_i32, _i32, _vp, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _vp]),
         "orc_tri_grid": (None, [_vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp]),
         "orc_sphere_grid": (None, [_vp, _f32, _vp, _i32, _i32, _i32, _i32, _vp]),
+        "orc_tri_t_grid": (None, [_vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp]),
         "orc_fnv1a_i32": (ctypes.c_uint64, [_vp, ctypes.c_int64]),
         "orc_libm_sincosf": (None, [_vp, ctypes.c_int64, _vp, _vp]),
         "orc_pack_rgba8": (None, [_vp, ctypes.c_int64, _vp]),
@@ -179,6 +180,14 @@ class Oracle:
         d = np.ascontiguousarray(direction, np.float32)
         out = np.zeros((h, w), np.uint8)
         self.lib.orc_tri_grid(_p(a[0]), _p(a[1]), _p(a[2]), _p(d), x0, y0, w, h, _p(out))
+        return out
+
+    def tri_t_grid(self, v0, v1, v2, direction, x0, y0, w, h) -> np.ndarray:
+        """The reference's fp64 t per pixel of the w x h grid (NaN = miss)."""
+        a = [np.ascontiguousarray(v, np.float32)[:3].copy() for v in (v0, v1, v2)]
+        d = np.ascontiguousarray(direction, np.float32)
+        out = np.zeros((h, w), np.float64)
+        self.lib.orc_tri_t_grid(_p(a[0]), _p(a[1]), _p(a[2]), _p(d), x0, y0, w, h, _p(out))
         return out
 
     def sphere_grid(self, centre, radius, direction, x0, y0, w, h) -> np.ndarray:

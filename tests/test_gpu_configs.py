@@ -167,27 +167,43 @@ def _tie_scene(pkg, w, h, n, seed):
     return pkg.Scene(so, r, sc)
 
 
-@pytest.mark.parametrize("case", ["dense", "dense_rgba8", "ties", "cubes_and_spheres"])
+@pytest.mark.parametrize("case", ["dense", "dense_rgba8", "ties", "cubes_and_spheres",
+                                  "dense_cubes", "heavy_defaults"])
 def test_coarse_depth_cull_exact(pkg, rt, oracle, case):
     """The coarse kernel's depth cull (per-tile cover bounds) drops only
-    spheres that cannot win a pixel: frames with it on and off are
+    candidates that cannot win a pixel: frames with it on and off are
     identical and equal the oracle, in the dense regime where it drops most
-    and with exact ties."""
+    and with exact ties.  "heavy_defaults": a scene of 16x config 3's object
+    density, whose box overdraw (about 40) passes the library's default
+    triangle gate, rendered with the defaults."""
     fmt = "rgba8" if case.endswith("rgba8") else "i32x4"
     w, h = 640, 480
     if case == "ties":
         scene = _tie_scene(pkg, w, h, 400, 3)
     elif case == "cubes_and_spheres":
         scene = pkg.Scene.synthetic(w, h, 300, 40, seed=9, k=w / 640 * 4)
+    elif case == "dense_cubes":  # triangles cover and drop each other
+        scene = pkg.Scene.synthetic(w, h, 60, 200, seed=10, k=w / 640 * 3)
+    elif case == "heavy_defaults":  # config 3's scene generator at 16x the objects
+        scene = pkg.Scene.synthetic(w, h, 4096, 1024, seed=3, k=6.4 * w / 4096)
     else:
         scene = pkg.Scene.synthetic(w, h, 1200, 0, seed=5, k=w / 640 * 4)
     try:
         rt.set_coarse_cull(0)
+        rt.set_coarse_cull_tri(0)
         off, _ = rt.render(scene, w, h, fmt=fmt)
-        rt.set_coarse_cull(1)  # every bin
+        if case == "heavy_defaults":
+            rt.set_coarse_cull(-1)
+            rt.set_coarse_cull_tri(-1)
+        else:
+            rt.set_coarse_cull(1)  # every bin, spheres and triangles, every frame
+            rt.set_coarse_cull_tri(1)
+            rt.set_coarse_cull_overdraw(0)
         on, t = rt.render(scene, w, h, fmt=fmt)
     finally:
-        rt.set_coarse_cull(-1)  # the library default
+        rt.set_coarse_cull(-1)  # the library defaults
+        rt.set_coarse_cull_tri(-1)
+        rt.set_coarse_cull_overdraw(-1)
     assert t.path == "binned"
     assert np.array_equal(on, off)
     want = oracle.trace(scene, w, h, threads=THREADS)

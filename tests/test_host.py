@@ -209,6 +209,40 @@ def test_triangle_box_and_tile_classifier_are_conservative(pkg, oracle, band, bu
     assert n_inside_tiles > 0 and n_skip_tiles > 0  # the classifier does something
 
 
+@pytest.mark.parametrize("tile", [(16, 16), (64, 4)])
+def test_triangle_t_bounds_hold(pkg, oracle, tile):
+    """The coarse depth cull's triangle bounds (tri_t_bounds): for every
+    hitting pixel of a tile, the reference's fp64 t lies in [lo, hi], so its
+    float closest value lies in [(float)lo, (float)hi] -- the property the
+    cull's strict comparisons rely on.  Random, sliver, tiny, huge and
+    axis-aligned triangles; tiles of both wave-tile shapes around them."""
+    w, h = 176, 160
+    tw, th = tile
+    rng = np.random.default_rng(29 + tw)
+    n_checked = 0
+    for v in random_triangles(rng, w, h, 150):
+        ok, box, _ = pkg.debug_triangle_prep(v[0], v[1], v[2], RAY_DIR, w, 0, h)
+        if not ok or box[0] > box[2]:
+            continue
+        for _ in range(6):
+            tx = int(rng.integers(max(box[0] - tw, 0), box[2] + 1)) // tw * tw
+            ty = int(rng.integers(max(box[1] - th, 0), box[3] + 1)) // th * th
+            b = pkg.debug_triangle_t_bounds(v[0], v[1], v[2], RAY_DIR, w, 0, h,
+                                            tx, tx + tw - 1, ty, ty + th - 1)
+            if b is None:
+                continue
+            ts = oracle.tri_t_grid(v[0], v[1], v[2], RAY_DIR, tx, ty, tw, th)
+            hit = ~np.isnan(ts)
+            if not hit.any():
+                continue
+            lo, hi = b
+            assert (ts[hit] >= lo).all() and (ts[hit] <= hi).all(), (v, tx, ty, lo, hi)
+            f = ts[hit].astype(np.float32)
+            assert (f >= np.float32(lo)).all() and (f <= np.float32(hi)).all()
+            n_checked += int(hit.sum())
+    assert n_checked > 10000
+
+
 def test_sphere_box_and_tile_classifier_are_conservative(pkg, oracle):
     w, h = 160, 128
     shapes = classified_shapes(pkg)
