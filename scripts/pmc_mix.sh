@@ -1,5 +1,6 @@
 #!/bin/bash
 # Instruction-mix PMC passes for one library variant (LIB=...), kernel-trace only.
+# KERNEL=coarse3 aggregates that kernel instead of the trace.
 set -u
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$R"; mkdir -p gpurun_out; export TMPDIR=/tmp
@@ -17,13 +18,14 @@ for grp in "SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ
       python "$R/bench.py" $ARGS > "$R/gpurun_out/${TAG}_$i.log" 2>&1)
   rc=$?; echo "pass $i rc=$rc"; [ $rc -ne 0 ] && { tail -5 "$R/gpurun_out/${TAG}_$i.log"; exit $rc; }
 done
-python - "$R/gpurun_out" "$TAG" <<'PY'
+python - "$R/gpurun_out" "$TAG" "${KERNEL:-trace}" <<'PY'
 import csv, glob, sys, collections
-d, tag = sys.argv[1], sys.argv[2]
+d, tag, kern = sys.argv[1], sys.argv[2], sys.argv[3]
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in glob.glob(f"{d}/{tag}_*/run_counter_collection.csv"):
     for r in csv.DictReader(open(f)):
-        if "trace3_kernel" in r["Kernel_Name"] or "trace_kernel" in r["Kernel_Name"]:
+        name = r["Kernel_Name"]
+        if (kern in name) if kern != "trace" else ("trace3_kernel" in name or "trace_kernel" in name):
             agg["trace"][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, v in sorted(agg["trace"].items()):
     print(f"{k:28s} {sum(v)/len(v):14.0f}")

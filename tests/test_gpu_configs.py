@@ -167,8 +167,20 @@ def _tie_scene(pkg, w, h, n, seed):
     return pkg.Scene(so, r, sc)
 
 
+def _cube_tie_scene(pkg, w, h, seed):
+    """Dense cubes plus exact duplicates recoloured (their triangles tie at
+    every pixel: the first cube must win, MainState.cpp:386-391), and a few
+    spheres."""
+    base = pkg.Scene.synthetic(w, h, 30, 160, seed=seed, k=w / 640 * 3)
+    rng = np.random.default_rng(seed)
+    dup = rng.choice(len(base.cube_vertices), 40, replace=False)
+    cv = np.concatenate([base.cube_vertices, base.cube_vertices[dup]])
+    cc = np.concatenate([base.cube_colours, base.cube_colours[dup][:, [2, 0, 1, 3]]])
+    return pkg.Scene(base.sphere_origins, base.sphere_radius, base.sphere_colours, cv, cc)
+
+
 @pytest.mark.parametrize("case", ["dense", "dense_rgba8", "ties", "cubes_and_spheres",
-                                  "dense_cubes", "heavy_defaults"])
+                                  "dense_cubes", "cube_ties", "heavy_defaults"])
 def test_coarse_depth_cull_exact(pkg, rt, oracle, case):
     """The coarse kernel's depth cull (per-tile cover bounds) drops only
     candidates that cannot win a pixel: frames with it on and off are
@@ -184,6 +196,8 @@ def test_coarse_depth_cull_exact(pkg, rt, oracle, case):
         scene = pkg.Scene.synthetic(w, h, 300, 40, seed=9, k=w / 640 * 4)
     elif case == "dense_cubes":  # triangles cover and drop each other
         scene = pkg.Scene.synthetic(w, h, 60, 200, seed=10, k=w / 640 * 3)
+    elif case == "cube_ties":
+        scene = _cube_tie_scene(pkg, w, h, 12)
     elif case == "heavy_defaults":  # config 3's scene generator at 16x the objects
         scene = pkg.Scene.synthetic(w, h, 4096, 1024, seed=3, k=6.4 * w / 4096)
     else:
