@@ -76,6 +76,7 @@ struct rt_ctx {
     void* list_buf = nullptr;   size_t list_cap = 0;    // coarse-bin candidate lists
     unsigned* flag = nullptr;   // non-finite scene flag (generation-stamped)
     unsigned gen = 0;
+    unsigned od_launches = 0;  // binned launches: picks the box-overdraw slot
     int trace_mode = 0;  // diagnostics ablation, see trace3_kernel
     int tile_variant = 0;  // 0 = by frame size, 1 = 16x16 tiles, 2 = 64x4 tiles
     // coarse lists take 4 B x kListStride x (primitives + 16) per 64x64 bin; a frame whose
@@ -279,10 +280,10 @@ int rt_init(int device_ordinal, rt_ctx** out_ctx) {
             return RT_ERR_HIP;
         }
     }
-    // [0] non-finite flag, [1] explicit-origin grid check, [2..3] the frame's
-    // box overdraw (generation-stamped, see prep_kernel)
-    if (hipMalloc(&ctx->flag, 4 * sizeof(unsigned)) != hipSuccess ||
-        hipMemset(ctx->flag, 0, 4 * sizeof(unsigned)) != hipSuccess) {
+    // [0] non-finite flag, [1] explicit-origin grid check, [2..5] two
+    // 64-bit box-overdraw slots (see launch())
+    if (hipMalloc(&ctx->flag, 8 * sizeof(unsigned)) != hipSuccess ||
+        hipMemset(ctx->flag, 0, 8 * sizeof(unsigned)) != hipSuccess) {
         rt_destroy(ctx);
         return RT_ERR_OUT_OF_MEMORY;
     }

@@ -33,6 +33,8 @@ def main():
                     help="render rank 0's band of a frame and scene scaled for this many ranks "
                          "(bench.py's weak-scaling workload)")
     ap.add_argument("--format", default="i32x4", choices=("i32x4", "rgba8"))
+    ap.add_argument("--kernels", action="store_true",
+                    help="also per-kernel medians (rt_profile_*: HIP events on each kernel)")
     ap.add_argument("--modes", default="0",
                     help="comma list of trace-kernel ablation modes to time (0 = real)")
     args = ap.parse_args()
@@ -99,6 +101,20 @@ def main():
                     e0.elapsed_time(e1) / args.steps * 1e3)
     res = {n: {"median_us": round(statistics.median(v), 2), "min_us": round(min(v), 2)}
            for n, v in times.items()}
+    if args.kernels:
+        dbl = ctypes.c_double
+        for name, lib, ctx in libs:
+            ks = {"prep": [], "bin": [], "trace": []}
+            for _ in range(args.rounds):
+                lib.rt_profile_enable(ctx, 1)
+                run(lib, ctx, args.steps)
+                v = [dbl(), dbl(), dbl()]
+                n = ctypes.c_int32()
+                assert lib.rt_profile_read(ctx, *[ctypes.byref(x) for x in v], ctypes.byref(n)) == 0
+                lib.rt_profile_enable(ctx, 0)
+                for key, x in zip(ks, v):
+                    ks[key].append(x.value * 1e3 / max(n.value, 1))
+            res[name].update({f"{key}_us": round(statistics.median(x), 2) for key, x in ks.items()})
     print(json.dumps(res, indent=1))
 
 
