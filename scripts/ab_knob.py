@@ -21,7 +21,13 @@ sys.path.insert(0, str(REPO))
 
 # name: (width, frame height, rendered rows, spheres, cubes, seed, k)
 CONFIGS = {
+    "c1": (512, 512, (0, 512), 4, 1, 1, 0.8),
     "c2": (1920, 1080, (0, 1080), 16, 4, 2, 3.0),
+    # reference scene 2's size: 640x480, 8 spheres + 10 cubes
+    "s2": (640, 480, (0, 480), 8, 10, 1, 1.0),
+    # 1080p with 256 / 512 primitives (the small path's 4- and 8-chunk instances)
+    "p256": (1920, 1080, (0, 1080), 64, 16, 2, 3.0),
+    "p512": (1920, 1080, (0, 1080), 128, 32, 2, 3.0),
     "c3": (4096, 4096, (0, 4096), 256, 64, 3, 6.4),
     "c3s": (4096, 4096, (0, 4096), 256, 64, 3, 1.0),
     "c4": (8192, 8192, (0, 8192), 192, 64, 4, 12.8),
@@ -39,7 +45,8 @@ CONFIGS = {
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--knob", default="coarse_cull",
-                    choices=("coarse_cull", "coarse_cull_tri", "coarse_cull_overdraw", "small_path", "bin_masks",
+                    choices=("coarse_cull", "coarse_cull_tri", "coarse_cull_overdraw", "tile_variant",
+                             "small_path", "bin_masks",
                              "trace_mode"))
     ap.add_argument("--values", default="0,1")
     ap.add_argument("--configs", default="c3,c5d,c5s,band8")
@@ -58,6 +65,7 @@ def main():
     rt = pkg.RayTracer(0)
     setter = {"coarse_cull": rt.set_coarse_cull, "coarse_cull_tri": rt.set_coarse_cull_tri,
               "coarse_cull_overdraw": rt.set_coarse_cull_overdraw,
+              "tile_variant": rt.set_tile_variant,
               "small_path": rt.set_small_path,
               "bin_masks": rt.set_bin_masks, "trace_mode": rt.set_trace_mode}[args.knob]
     values = [int(v) for v in args.values.split(",")]

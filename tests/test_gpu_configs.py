@@ -73,6 +73,35 @@ def test_config5_full_frame(pkg, rt, oracle):
     _full_frame_vs_oracle(pkg, rt, oracle, 16384, h, 4096, 0, 5, rows, bands=8)
 
 
+@pytest.mark.parametrize("config", ["config4", "config5"])
+def test_full_size_rgba8_is_packed_i32x4(pkg, rt, config):
+    """The Texture (RGBA8) frame at BASELINE's full sizes equals the byte
+    pack of the int32x4 frame (MainState.cpp:1026-1036: each channel's low
+    byte, alpha 0xFF) at every pixel -- a size-independent property that
+    carries the int32x4 oracle parity of the config 4 / 5 tests above to the
+    second output format."""
+    torch = pytest.importorskip("torch")
+    w, ns, nc, seed = (8192, 192, 64, 4) if config == "config4" else (16384, 4096, 0, 5)
+    h = w
+    dev = torch.device("cuda:0")
+    scene = pkg.Scene.synthetic(w, h, ns, nc, seed=seed, k=w / 640)
+    keep, ds = _device_scene(torch, scene, dev)
+    stream = torch.cuda.current_stream().cuda_stream
+    full = torch.empty((h, w, 4), dtype=torch.int32, device=dev)
+    tex = torch.empty((h, w), dtype=torch.int32, device=dev)
+    rt.render_device(ds, w, h, (0, h), full.data_ptr(), stream=stream)
+    rt.render_device(ds, w, h, (0, h), tex.data_ptr(), fmt="rgba8", stream=stream)
+    torch.cuda.synchronize()
+    alpha = torch.tensor(-16777216, dtype=torch.int32, device=dev)  # 0xFF000000
+    for r0 in range(0, h, 1024):
+        f = full[r0:r0 + 1024]
+        packed = ((f[..., 0] & 255) | ((f[..., 1] & 255) << 8) | ((f[..., 2] & 255) << 16)
+                  | alpha)
+        bad = int((packed != tex[r0:r0 + 1024]).sum())
+        assert bad == 0, f"rows {r0}..{r0 + 1024}: {bad} pixels differ"
+    del full, tex, keep
+
+
 def test_render_multi_explicit_origins_band_upload(pkg, rt, oracle):
     """rt_render_multi with explicit origins: each band uploads only its own
     rows of the origin array (MainState.cpp:841-855 uploads them all) and
