@@ -155,6 +155,7 @@ def library() -> ctypes.CDLL:
         "rt_debug_set_tile_variant": (ctypes.c_int, [vp, ctypes.c_int]),
         "rt_debug_set_coarse_cull_tri": (ctypes.c_int, [vp, ctypes.c_int]),
         "rt_debug_set_coarse_cull_overdraw": (ctypes.c_int, [vp, ctypes.c_int]),
+        "rt_debug_set_small_fused": (ctypes.c_int, [vp, ctypes.c_int]),
         "rt_debug_triangle_t_bounds": (ctypes.c_int, [vp, vp, vp, vp, i32, i32, i32, i32, i32,
                                                       i32, i32, vp]),
         "rt_debug_triangle_box_wide": (ctypes.c_int, [vp, vp, vp, vp, i32, i32, i32, vp, vp]),
@@ -509,6 +510,12 @@ class RayTracer:
         general prep -> coarse -> trace path (diagnostics / tests)."""
         _check(library().rt_debug_set_small_path(self._ctx, int(enable)),
                "rt_debug_set_small_path")
+
+    def set_small_fused(self, enable: bool) -> None:
+        """Scenes of at most 128 primitives: the one-kernel frame_small_kernel
+        (default) or prep + trace_small_kernel (diagnostics / tests)."""
+        _check(library().rt_debug_set_small_fused(self._ctx, int(enable)),
+               "rt_debug_set_small_fused")
 
     def set_coarse_cull_tri(self, min_candidates: int) -> None:
         """Diagnostics: triangles join the coarse depth cull in bins with at

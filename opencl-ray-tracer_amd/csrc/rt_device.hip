@@ -57,6 +57,9 @@
 #define RT_COARSE_CULL_TRI 4  // default of rt_debug_set_coarse_cull_tri: triangles join the cull
                               // in bins whose tiles keep >= this many candidates on average
 #endif
+#ifndef RT_SMALL_FUSED
+#define RT_SMALL_FUSED 1  // default of rt_debug_set_small_fused
+#endif
 #ifndef RT_COARSE_CULL_OVERDRAW
 #define RT_COARSE_CULL_OVERDRAW 5  // default of rt_debug_set_coarse_cull_overdraw: ... in frames
                                    // whose primitive boxes cover the frame >= 5 times
@@ -84,6 +87,7 @@ struct rt_ctx {
     int64_t list_budget = (int64_t)4 << 30;
     bool bin_masks = RT_BIN_MASKS != 0;  // separable bin masks (false: coarse scans every box)
     bool small_path = true;  // <= 64 x RT_SMALL_CHUNKS primitives: trace_small_kernel
+    bool small_fused = RT_SMALL_FUSED != 0;  // <= 64 x RT_FUSED_CHUNKS primitives: frame_small_kernel
     // coarse depth cull of sphere candidates in bins with at least this many
     // candidates (0 = off)
     int coarse_cull = RT_COARSE_CULL;
@@ -667,6 +671,12 @@ int rt_debug_triangle_t_bounds(const float v0[3], const float v1[3], const float
                        &bad, &d))
         return 0;
     return tri_t_bounds(d, xa, xb, ya, yb, &out[0], &out[1]) ? 1 : 0;
+}
+
+int rt_debug_set_small_fused(rt_ctx* ctx, int enable) {
+    if (!ctx) return RT_ERR_INVALID_ARG;
+    ctx->small_fused = enable != 0;
+    return RT_OK;
 }
 
 int rt_debug_set_small_path(rt_ctx* ctx, int enable) {

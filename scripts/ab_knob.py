@@ -46,6 +46,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--knob", default="coarse_cull",
                     choices=("coarse_cull", "coarse_cull_tri", "coarse_cull_overdraw", "tile_variant",
+                             "small_fused",
                              "small_path", "bin_masks",
                              "trace_mode"))
     ap.add_argument("--values", default="0,1")
@@ -66,6 +67,7 @@ def main():
     setter = {"coarse_cull": rt.set_coarse_cull, "coarse_cull_tri": rt.set_coarse_cull_tri,
               "coarse_cull_overdraw": rt.set_coarse_cull_overdraw,
               "tile_variant": rt.set_tile_variant,
+              "small_fused": rt.set_small_fused,
               "small_path": rt.set_small_path,
               "bin_masks": rt.set_bin_masks, "trace_mode": rt.set_trace_mode}[args.knob]
     values = [int(v) for v in args.values.split(",")]

@@ -217,13 +217,27 @@ def test_nonfinite_scene_falls_back_exactly(pkg, rt, oracle):
     scene.cube_vertices[0, 4, 0] = np.nan
     want = oracle.trace(scene, 90, 70)
     try:
-        for small in (True, False):
+        for small, fused in ((True, True), (True, False), (False, False)):
             rt.set_small_path(small)
+            rt.set_small_fused(fused)
             got, t = rt.render(scene, 90, 70)
             assert t.path == "binned"
-            assert np.array_equal(got, want), small
+            assert np.array_equal(got, want), (small, fused)
     finally:
         rt.set_small_path(True)
+        rt.set_small_fused(True)
+    # a second chunk's primitive non-finite (frame_small_kernel's second
+    # prep wave)
+    big = pkg.Scene.synthetic(90, 70, 100, 0, seed=4, k=0.2)
+    big.sphere_radius[90] = np.nan
+    want = oracle.trace(big, 90, 70)
+    try:
+        for fused in (True, False):
+            rt.set_small_fused(fused)
+            got, _ = rt.render(big, 90, 70)
+            assert np.array_equal(got, want), fused
+    finally:
+        rt.set_small_fused(True)
 
 
 @pytest.mark.parametrize("w,h,ns,nc,k", [(512, 512, 4, 1, 1.0), (1920, 1080, 16, 4, 3.0),
@@ -235,25 +249,30 @@ def test_nonfinite_scene_falls_back_exactly(pkg, rt, oracle):
                                          (1111, 999, 300, 10, 2.0), (3000, 700, 512, 0, 3.0)])
 def test_small_scene_path(pkg, rt, oracle, w, h, ns, nc, k):
     """<= 512 primitives (up to 8 prep chunks): trace_small_kernel classifies
-    each tile's candidates itself.  Same frames as the general path and the
-    oracle, whole frames, row bands and the Texture format; 513 primitives
-    take the general path."""
+    each tile's candidates itself; <= 128 primitives: frame_small_kernel does
+    prep, classification and trace in one kernel.  Same frames from all
+    three and the general path and the oracle, whole frames, row bands and
+    the Texture format; 513 primitives take the general path."""
     scene = pkg.Scene.synthetic(w, h, ns, nc, seed=w + ns, k=k)
     assert ns + 12 * nc <= 512
     frames = {}
     try:
-        for small in (True, False):
+        for small, fused in ((True, True), (True, False), (False, False)):
             rt.set_small_path(small)
+            rt.set_small_fused(fused)
             full, t = rt.render(scene, w, h)
             assert t.path == "binned"
             band, _ = rt.render(scene, w, h, rows=(h // 3, h - h // 5))
             assert np.array_equal(band, full[h // 3:h - h // 5])
             tex, _ = rt.render(scene, w, h, fmt="rgba8")
             assert np.array_equal(tex, pkg.pack_rgba8(full))
-            frames[small] = full
+            frames[small, fused] = full
     finally:
         rt.set_small_path(True)
-    assert np.array_equal(frames[True], frames[False])
+        rt.set_small_fused(True)
+    assert np.array_equal(frames[True, True], frames[False, False])
+    assert np.array_equal(frames[True, False], frames[False, False])
+    frames[True] = frames[True, True]
     want = oracle.trace(scene, w, h, threads=THREADS)
     assert not diff_report(frames[True], want), diff_report(frames[True], want)
     # one more primitive: the general path
@@ -628,16 +647,21 @@ def test_list_budget_bands(pkg, rt, oracle):
 
 
 def test_profile_slots_of_skipped_kernels(pkg, rt):
-    """Per-kernel profiling: a kernel that does not run reads 0 ms (small
-    scenes skip the coarse kernel, empty scenes prep and coarse, the generic
-    path both), the kernels that run read > 0."""
+    """Per-kernel profiling: a kernel that does not run reads 0 ms (scenes of
+    at most 128 primitives run one kernel, frame_small_kernel, in the trace
+    slot; with it off, prep + trace_small_kernel skip the coarse kernel;
+    empty scenes skip prep and coarse, the generic path both), the kernels
+    that run read > 0."""
     small = pkg.Scene.synthetic(640, 480, 8, 2, seed=2, k=1.0)
     big = pkg.Scene.synthetic(640, 480, 500, 10, seed=2, k=1.0)
-    cases = [(small, "binned", (True, False, True)), (big, "binned", (True, True, True)),
-             (pkg.Scene(), "binned", (False, False, True)),
-             (small, "generic", (False, False, True))]
+    cases = [(small, "binned", (False, False, True), True),
+             (small, "binned", (True, False, True), False),
+             (big, "binned", (True, True, True), True),
+             (pkg.Scene(), "binned", (False, False, True), True),
+             (small, "generic", (False, False, True), True)]
     try:
-        for scene, path, ran in cases:
+        for scene, path, ran, fused in cases:
+            rt.set_small_fused(fused)
             rt.profile(True)
             rt.render(scene, 640, 480, path=path)
             rt.render(scene, 640, 480, path=path)
@@ -648,6 +672,7 @@ def test_profile_slots_of_skipped_kernels(pkg, rt):
                 assert (prof[key] > 0) == on, (path, key, prof)
     finally:
         rt.profile(False)
+        rt.set_small_fused(True)
 
 
 @pytest.mark.parametrize("n_ctx", [1, 2, 3, 5])
