@@ -64,8 +64,9 @@ int rt_debug_set_bin_masks(rt_ctx* ctx, int enable);
  * general prep -> coarse -> trace path. */
 int rt_debug_set_small_path(rt_ctx* ctx, int enable);
 /* Scenes of at most 128 primitives: 1 (default) = frame_small_kernel (prep,
- * classification and trace in one kernel, records in LDS), 0 = prep_kernel +
- * trace_small_kernel (A/B and tests).  Needs the small path (above). */
+ * classification and trace in one kernel, records in LDS) on frames whose
+ * grid is resident at once, 2 = on every frame size (tests), 0 = prep_kernel
+ * + trace_small_kernel (A/B and tests).  Needs the small path (above). */
 int rt_debug_set_small_fused(rt_ctx* ctx, int enable);
 /* Coarse depth cull of sphere candidates in coarse bins with at least
  * `enable` sphere candidates (1 = every bin, 0 = off: every candidate the tile

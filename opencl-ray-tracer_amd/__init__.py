@@ -511,10 +511,11 @@ class RayTracer:
         _check(library().rt_debug_set_small_path(self._ctx, int(enable)),
                "rt_debug_set_small_path")
 
-    def set_small_fused(self, enable: bool) -> None:
+    def set_small_fused(self, mode: int) -> None:
         """Scenes of at most 128 primitives: the one-kernel frame_small_kernel
-        (default) or prep + trace_small_kernel (diagnostics / tests)."""
-        _check(library().rt_debug_set_small_fused(self._ctx, int(enable)),
+        where its grid is resident at once (1, default), on every frame size
+        (2), or prep + trace_small_kernel (0) (diagnostics / tests)."""
+        _check(library().rt_debug_set_small_fused(self._ctx, int(mode)),
                "rt_debug_set_small_fused")
 
     def set_coarse_cull_tri(self, min_candidates: int) -> None:

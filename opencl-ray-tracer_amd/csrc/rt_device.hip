@@ -87,7 +87,10 @@ struct rt_ctx {
     int64_t list_budget = (int64_t)4 << 30;
     bool bin_masks = RT_BIN_MASKS != 0;  // separable bin masks (false: coarse scans every box)
     bool small_path = true;  // <= 64 x RT_SMALL_CHUNKS primitives: trace_small_kernel
-    bool small_fused = RT_SMALL_FUSED != 0;  // <= 64 x RT_FUSED_CHUNKS primitives: frame_small_kernel
+    // <= 64 x RT_FUSED_CHUNKS primitives on frames whose grid is resident at
+    // once: frame_small_kernel (1; 2 = on every frame size, tests; 0 = off)
+    int small_fused = RT_SMALL_FUSED;
+    int n_cu = 256;  // compute units (rt_init)
     // coarse depth cull of sphere candidates in bins with at least this many
     // candidates (0 = off)
     int coarse_cull = RT_COARSE_CULL;
@@ -274,6 +277,9 @@ int rt_init(int device_ordinal, rt_ctx** out_ctx) {
     if (hipSetDevice(device_ordinal) != hipSuccess) return RT_ERR_HIP;
     rt_ctx* ctx = new rt_ctx();
     ctx->device = device_ordinal;
+    if (hipDeviceGetAttribute(&ctx->n_cu, hipDeviceAttributeMultiprocessorCount,
+                              device_ordinal) != hipSuccess || ctx->n_cu <= 0)
+        ctx->n_cu = 256;
     if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
         delete ctx;
         return RT_ERR_HIP;
@@ -674,8 +680,8 @@ int rt_debug_triangle_t_bounds(const float v0[3], const float v1[3], const float
 }
 
 int rt_debug_set_small_fused(rt_ctx* ctx, int enable) {
-    if (!ctx) return RT_ERR_INVALID_ARG;
-    ctx->small_fused = enable != 0;
+    if (!ctx || enable < 0 || enable > 2) return RT_ERR_INVALID_ARG;
+    ctx->small_fused = enable;
     return RT_OK;
 }
 

@@ -28,6 +28,11 @@ CONFIGS = {
     # 1080p with 256 / 512 primitives (the small path's 4- and 8-chunk instances)
     "p256": (1920, 1080, (0, 1080), 64, 16, 2, 3.0),
     "p512": (1920, 1080, (0, 1080), 128, 32, 2, 3.0),
+    # small scenes on large frames (the one-kernel path's prep per workgroup)
+    "uhd64": (3840, 2160, (0, 2160), 16, 4, 2, 6.0),
+    "c3s64": (4096, 4096, (0, 4096), 16, 4, 3, 6.4),
+    "c4s64": (8192, 8192, (0, 8192), 16, 4, 4, 12.8),
+    "c3s16": (4096, 4096, (0, 4096), 4, 1, 1, 6.4),
     "c3": (4096, 4096, (0, 4096), 256, 64, 3, 6.4),
     "c3s": (4096, 4096, (0, 4096), 256, 64, 3, 1.0),
     "c4": (8192, 8192, (0, 8192), 192, 64, 4, 12.8),

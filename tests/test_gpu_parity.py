@@ -219,13 +219,13 @@ def test_nonfinite_scene_falls_back_exactly(pkg, rt, oracle):
     try:
         for small, fused in ((True, True), (True, False), (False, False)):
             rt.set_small_path(small)
-            rt.set_small_fused(fused)
+            rt.set_small_fused(2 if fused else 0)
             got, t = rt.render(scene, 90, 70)
             assert t.path == "binned"
             assert np.array_equal(got, want), (small, fused)
     finally:
         rt.set_small_path(True)
-        rt.set_small_fused(True)
+        rt.set_small_fused(1)
     # a second chunk's primitive non-finite (frame_small_kernel's second
     # prep wave)
     big = pkg.Scene.synthetic(90, 70, 100, 0, seed=4, k=0.2)
@@ -233,11 +233,11 @@ def test_nonfinite_scene_falls_back_exactly(pkg, rt, oracle):
     want = oracle.trace(big, 90, 70)
     try:
         for fused in (True, False):
-            rt.set_small_fused(fused)
+            rt.set_small_fused(2 if fused else 0)
             got, _ = rt.render(big, 90, 70)
             assert np.array_equal(got, want), fused
     finally:
-        rt.set_small_fused(True)
+        rt.set_small_fused(1)
 
 
 @pytest.mark.parametrize("w,h,ns,nc,k", [(512, 512, 4, 1, 1.0), (1920, 1080, 16, 4, 3.0),
@@ -259,7 +259,7 @@ def test_small_scene_path(pkg, rt, oracle, w, h, ns, nc, k):
     try:
         for small, fused in ((True, True), (True, False), (False, False)):
             rt.set_small_path(small)
-            rt.set_small_fused(fused)
+            rt.set_small_fused(2 if fused else 0)
             full, t = rt.render(scene, w, h)
             assert t.path == "binned"
             band, _ = rt.render(scene, w, h, rows=(h // 3, h - h // 5))
@@ -269,7 +269,7 @@ def test_small_scene_path(pkg, rt, oracle, w, h, ns, nc, k):
             frames[small, fused] = full
     finally:
         rt.set_small_path(True)
-        rt.set_small_fused(True)
+        rt.set_small_fused(1)
     assert np.array_equal(frames[True, True], frames[False, False])
     assert np.array_equal(frames[True, False], frames[False, False])
     frames[True] = frames[True, True]
@@ -661,7 +661,7 @@ def test_profile_slots_of_skipped_kernels(pkg, rt):
              (small, "generic", (False, False, True), True)]
     try:
         for scene, path, ran, fused in cases:
-            rt.set_small_fused(fused)
+            rt.set_small_fused(2 if fused else 0)
             rt.profile(True)
             rt.render(scene, 640, 480, path=path)
             rt.render(scene, 640, 480, path=path)
@@ -672,7 +672,7 @@ def test_profile_slots_of_skipped_kernels(pkg, rt):
                 assert (prof[key] > 0) == on, (path, key, prof)
     finally:
         rt.profile(False)
-        rt.set_small_fused(True)
+        rt.set_small_fused(1)
 
 
 @pytest.mark.parametrize("n_ctx", [1, 2, 3, 5])
