@@ -184,7 +184,7 @@ int skip_k(rt_ctx* ctx, const hipEvent_t* ev) {
 }  // namespace
 
 // The kernels and launch(), once per wave-tile shape (rt_trace.inc).
-// 16x16 tiles suit frames up to 1 GiB; larger frames store faster from
+// 16x16 tiles suit frames below 512 MiB; larger frames store faster from
 // 64x4 tiles ("Wave tile shape per frame size").
 #ifndef RT_TILE_NARROW
 #define RT_TILE_NARROW 16
@@ -232,8 +232,11 @@ __global__ void __launch_bounds__(256) grid_check_kernel(const float4* __restric
     if (__ballot(off) != 0ull && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
 }
 
-// Frames of at least this many bytes take the wide tiles (auto selection).
-constexpr int64_t kWideTileBytes = (int64_t)1 << 30;
+// Frames of at least this many bytes take the wide tiles (auto selection):
+// 512 MiB frames store faster from 64x4 tiles in both formats (config 5's
+// 8-rank band, config 4's half frame, a 512 MiB Texture), 384 MiB and
+// smaller ones from 16x16.
+constexpr int64_t kWideTileBytes = (int64_t)1 << 29;
 
 // rt_debug_set_tile_variant: 0 = by frame size, 1 = 16x16, 2 = 64x4
 int render_launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origins,

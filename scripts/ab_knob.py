@@ -40,6 +40,14 @@ CONFIGS = {
     "c5s": (16384, 16384, (0, 16384), 4096, 0, 5, 1.0),
     # rank 0's band of bench.py's 8-rank weak-scaling workload
     "band8": (4096, 32768, (0, 4096), 2048, 512, 3, 6.4),
+    # rank 0's bands of configs 4 and 5 (8 ranks)
+    "c4band": (8192, 8192, (0, 1024), 192, 64, 4, 12.8),
+    "c4half": (8192, 8192, (0, 4096), 192, 64, 4, 12.8),
+    "c4q3": (8192, 8192, (0, 3072), 192, 64, 4, 12.8),
+    "c5half": (16384, 16384, (0, 8192), 4096, 0, 5, 25.6),
+    "c5band4": (16384, 16384, (0, 4096), 4096, 0, 5, 25.6),
+    "c5dband": (16384, 16384, (0, 2048), 4096, 0, 5, 25.6),
+    "c5sband": (16384, 16384, (0, 2048), 4096, 0, 5, 1.0),
     # scenes of 4x and 16x config 3's object count at the same density
     "c3x4": (4096, 4096, (0, 4096), 1024, 256, 3, 6.4),
     "c3x16": (4096, 4096, (0, 4096), 4096, 1024, 3, 6.4),
