@@ -307,3 +307,39 @@ def test_wide_tile_build_exact(pkg, rt, oracle, case):
         assert np.array_equal(wide, want)
     finally:
         rt.set_tile_variant(0)
+
+
+@pytest.mark.parametrize("seed", list(range(64)))
+def test_randomized_parity_sweep(pkg, rt, oracle, seed):
+    """Seeded random frames against the oracle: frame sizes from 96 to 1500
+    px a side, 1 to 600 spheres and 0 to 80 cubes at random densities, row
+    bands, both formats, both tile builds, and the culls / small-scene paths
+    forced on or off -- every combination of the round's binned paths."""
+    rng = np.random.default_rng(1000 + seed)
+    w = int(rng.integers(96, 1500))
+    h = int(rng.integers(96, 1100))
+    ns = int(rng.integers(1, 600)) if seed % 4 else int(rng.integers(1, 40))
+    nc = int(rng.integers(0, 80)) if seed % 4 else int(rng.integers(0, 6))
+    k = float(rng.uniform(0.3, 6.0)) * w / 640
+    scene = pkg.Scene.synthetic(w, h, ns, nc, seed=seed, k=k)
+    rows = (0, h) if seed % 3 else (int(rng.integers(0, h // 2)), int(rng.integers(h // 2 + 1, h + 1)))
+    fmt = "rgba8" if seed % 5 == 0 else "i32x4"
+    try:
+        rt.set_tile_variant(1 + seed % 2)
+        rt.set_small_fused((2, 0, 1)[seed % 3])
+        if seed % 2:  # every depth cull forced on, in every bin and frame
+            rt.set_coarse_cull(1)
+            rt.set_coarse_cull_tri(1)
+            rt.set_coarse_cull_overdraw(0)
+        got, t = rt.render(scene, w, h, rows=rows, fmt=fmt)
+    finally:
+        rt.set_tile_variant(0)
+        rt.set_small_fused(1)
+        rt.set_coarse_cull(-1)
+        rt.set_coarse_cull_tri(-1)
+        rt.set_coarse_cull_overdraw(-1)
+    assert t.path == "binned"
+    want = oracle.trace(scene, w, h, rows=rows, threads=THREADS)
+    if fmt == "rgba8":
+        want = oracle.pack_rgba8(want)
+    assert np.array_equal(got, want), (seed, w, h, ns, nc, k, rows, fmt)
