@@ -65,6 +65,8 @@ def main():
     ap.add_argument("--values", default="0,1")
     ap.add_argument("--configs", default="c3,c5d,c5s,band8")
     ap.add_argument("--format", default="i32x4", choices=("i32x4", "rgba8"))
+    ap.add_argument("--fixed", action="append", default=[],
+                    help="knob=value held for every setting (repeatable)")
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--no-check", action="store_true",
@@ -83,6 +85,14 @@ def main():
               "small_fused": rt.set_small_fused,
               "small_path": rt.set_small_path,
               "bin_masks": rt.set_bin_masks, "trace_mode": rt.set_trace_mode}[args.knob]
+    setters = {"coarse_cull": rt.set_coarse_cull, "coarse_cull_tri": rt.set_coarse_cull_tri,
+               "coarse_cull_overdraw": rt.set_coarse_cull_overdraw,
+               "tile_variant": rt.set_tile_variant, "small_fused": rt.set_small_fused,
+               "small_path": rt.set_small_path, "bin_masks": rt.set_bin_masks,
+               "trace_mode": rt.set_trace_mode}
+    for kv in args.fixed:
+        name, val = kv.split("=")
+        setters[name](int(val))
     values = [int(v) for v in args.values.split(",")]
     for cname in args.configs.split(","):
         w, h, (rb, re), ns, nc, seed, k = CONFIGS[cname]
@@ -124,7 +134,7 @@ def main():
                 rt.profile(False)
                 for key in kern[v]:
                     kern[v][key].append(p[key] * 1e3 / max(p["renders"], 1))
-        res = {"config": cname, "knob": args.knob, "format": args.format,
+        res = {"config": cname, "knob": args.knob, "format": args.format, "fixed": args.fixed,
                "frame": f"{w}x{h} rows {rb}..{re}, {ns}+{nc}, seed {seed}, k {k}"}
         for v in values:
             res[str(v)] = {"wall_us": round(statistics.median(walls[v]), 1),
