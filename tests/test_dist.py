@@ -56,7 +56,8 @@ def _worker(rank, world, port, width, height, scene_id, result_path, interleave=
 
 
 @pytest.mark.parametrize("height,scene_id,interleave", [(480, 1, 0), (97, 3, 0), (480, 1, 64),
-                                                       (200, 3, 64), (97, 2, 16)])
+                                                       (200, 3, 64), (97, 2, 16),
+                                                       (1, 1, 0), (1, 1, 64)])
 def test_two_rank_row_bands_gloo(tmp_path, oracle, height, scene_id, interleave):
     import torch.multiprocessing as mp
 
