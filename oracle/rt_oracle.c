@@ -22,6 +22,12 @@
  *   - scene random numbers: the reference's own misc/Random.cpp, compiled
  *     unmodified into oracle/_ref/libref_random.so, gives bit-identical
  *     Random::getFloat streams to orc_get_float below.
+ *   - the collide text (collide_mode: loop order, ties, the t0 == 0 skip,
+ *     shade, frame layout, the Moller-Trumbore text): the reference's own
+ *     OpenCL kernel rayTracer.cl, compiled unmodified for gfx950 into
+ *     oracle/_ref/rayTracer_gfx950.co and run on the GPU, equals
+ *     orc_trace_cl_gfx950 (the same text in the kernel's arithmetic) bit for
+ *     bit (tests/test_reference_kernel.py).
  */
 #include "rt_oracle.h"
 
@@ -425,26 +431,41 @@ void orc_scene_synthetic(int32_t width, int32_t height, int32_t n_spheres,
     dest[1] = v1[1] - v2[1]; \
     dest[2] = v1[2] - v2[2];
 
-/* MainState.cpp:257-298 (fp64 Moller-Trumbore, no t > 0 test) */
+/* Moller-Trumbore, MainState.cpp:257-298 (double: the parity target) and
+ * rayTracer.cl:37-78 (float: the reference's OpenCL kernel) are one source
+ * text with different types, so both are instantiated from one text here.
+ * No t > 0 test.  In the float instantiation `1.0 / det` divides in double
+ * and rounds to float, which equals the correctly rounded float quotient
+ * (53 >= 2 * 24 + 2: double rounding is innocuous for division); the
+ * EPSILON compare is made in double, as the kernel compiled for gfx950 does
+ * it (v_cvt_f64_f32 + v_cmp_*_f64). */
+#define DEFINE_MT(NAME, T)                                                        \
+    static int NAME(const T orig[3], const T dir[3], const T vert0[3],          \
+                    const T vert1[3], const T vert2[3], T* t, T* u, T* v) {      \
+        T edge1[3], edge2[3], tvec[3], pvec[3], qvec[3];                        \
+        T det, inv_det;                                                         \
+        SUB(edge1, vert1, vert0);                                               \
+        SUB(edge2, vert2, vert0);                                               \
+        CROSS(pvec, dir, edge2);                                                \
+        det = DOT(edge1, pvec);                                                 \
+        if (det > -EPSILON && det < EPSILON) return 0;                          \
+        inv_det = 1.0 / det;                                                    \
+        SUB(tvec, orig, vert0);                                                 \
+        *u = DOT(tvec, pvec) * inv_det;                                         \
+        if (*u < 0.0 || *u > 1.0) return 0;                                     \
+        CROSS(qvec, tvec, edge1);                                               \
+        *v = DOT(dir, qvec) * inv_det;                                          \
+        if (*v < 0.0 || *u + *v > 1.0) return 0;                                \
+        *t = DOT(edge2, qvec) * inv_det;                                        \
+        return 1;                                                               \
+    }
+DEFINE_MT(mt_f64, double)
+DEFINE_MT(mt_f32, float)
+
 int orc_intersect_tri(const double orig[3], const double dir[3], const double vert0[3],
                       const double vert1[3], const double vert2[3], double* t, double* u,
                       double* v) {
-    double edge1[3], edge2[3], tvec[3], pvec[3], qvec[3];
-    double det, inv_det;
-    SUB(edge1, vert1, vert0);
-    SUB(edge2, vert2, vert0);
-    CROSS(pvec, dir, edge2);
-    det = DOT(edge1, pvec);
-    if (det > -EPSILON && det < EPSILON) return 0;
-    inv_det = 1.0 / det;
-    SUB(tvec, orig, vert0);
-    *u = DOT(tvec, pvec) * inv_det;
-    if (*u < 0.0 || *u > 1.0) return 0;
-    CROSS(qvec, tvec, edge1);
-    *v = DOT(dir, qvec) * inv_det;
-    if (*v < 0.0 || *u + *v > 1.0) return 0;
-    *t = DOT(edge2, qvec) * inv_det;
-    return 1;
+    return mt_f64(orig, dir, vert0, vert1, vert2, t, u, v);
 }
 
 /* glm vec4 dot: (x0y0 + x1y1) + (x2y2 + x3y3), func_geometric.inl:75-81 */
@@ -453,18 +474,44 @@ static float dot4(const float a[4], const float b[4]) {
     return (t0 + t1) + (t2 + t3);
 }
 
-/* MainState.cpp:300-327 (fp32 through glm) */
-float orc_intersect_sphere(const float o[4], const float d[4], float radius,
-                           const float c[4]) {
+/* OpenCL's dot(float4, float4) as the ROCm device library implements it for
+ * gfx950 (the kernel's disassembly: v_mul_f32 then three v_fmac_f32, x to
+ * w): fma(a3, b3, fma(a2, b2, fma(a1, b1, a0 * b0))).  fmaf is exact in C. */
+static float dot4_cl(const float a[4], const float b[4]) {
+    return fmaf(a[3], b[3], fmaf(a[2], b[2], fmaf(a[1], b[1], a[0] * b[0])));
+}
+
+/* Which source the collide loop restates:
+ *  ORC_CPU        MainState.cpp:330-408 (fp64 triangles, glm dot, x86 (int))
+ *                 -- the parity target;
+ *  ORC_CL_GFX950  rayTracer.cl:111-202 as compiled for gfx950 with IEEE flags
+ *                 (oracle/Makefile): fp32 triangles, the device library's
+ *                 fma-chained dot, v_cvt_i32_f32 -- pinned bit-for-bit against
+ *                 that compiled kernel run on the GPU
+ *                 (tests/test_reference_kernel.py);
+ *  ORC_CL_X86     rayTracer.cl with glm's dot and x86 (int): the variant the
+ *                 survey's probe ran on the host (its CPU-vs-kernel counts). */
+enum { ORC_CPU = 0, ORC_CL_GFX950 = 1, ORC_CL_X86 = 2 };
+
+/* MainState.cpp:300-327 (fp32 through glm); rayTracer.cl:80-109 with the
+ * mode's dot */
+static inline __attribute__((always_inline)) float sphere_mode(int mode, const float o[4],
+                                                               const float d[4], float radius,
+                                                               const float c[4]) {
     float L[4] = {c[0] - o[0], c[1] - o[1], c[2] - o[2], c[3] - o[3]};
-    float tca = dot4(L, d);
+    float tca = mode == ORC_CL_GFX950 ? dot4_cl(L, d) : dot4(L, d);
     if (tca < 0) return 0.0f;
-    float distanceSquared = dot4(L, L) - tca * tca;
+    float distanceSquared = (mode == ORC_CL_GFX950 ? dot4_cl(L, L) : dot4(L, L)) - tca * tca;
     float radiusSquared = radius * radius;
     if (distanceSquared > radiusSquared) return 0.0f;
     float thc = sqrtf(radiusSquared - distanceSquared);
     float t0 = tca - thc;
     return t0;
+}
+
+float orc_intersect_sphere(const float o[4], const float d[4], float radius,
+                           const float c[4]) {
+    return sphere_mode(ORC_CPU, o, d, radius, c);
 }
 
 /* (int)f as x86-64 cvttss2si computes it (MainState.cpp:952-955):
@@ -474,37 +521,61 @@ static int32_t cvt_i32(float f) {
     return INT32_MIN;
 }
 
-/* MainState.cpp:330-408 */
-void orc_collide(const float origin[4], const float dir[4], int32_t n_spheres,
-                 const float* sphere_origins, const float* sphere_radius,
-                 const float* sphere_colours, int32_t n_cubes, const float* cube_vertices,
-                 const float* cube_colours, int32_t out[4]) {
+/* The kernel's int conversion on gfx950 (rayTracer.cl:198-201 -> 
+ * v_cvt_i32_f32): truncation, saturating at INT32_MIN / INT32_MAX, NaN -> 0. */
+static int32_t cvt_i32_amdgcn(float f) {
+    if (f != f) return 0;
+    if (f >= 2147483648.0f) return INT32_MAX;
+    if (f < -2147483648.0f) return INT32_MIN;
+    return (int32_t)f;
+}
+
+/* MainState.cpp:330-408 (rayTracer.cl:116-196 in the CL modes) */
+static inline __attribute__((always_inline)) void collide_mode(
+    int mode, const float origin[4], const float dir[4], int32_t n_spheres,
+    const float* sphere_origins, const float* sphere_radius, const float* sphere_colours,
+    int32_t n_cubes, const float* cube_vertices, const float* cube_colours, int32_t out[4]) {
     double rayOrigin[3] = {origin[0], origin[1], origin[2]};
     double rayDirection[3] = {dir[0], dir[1], dir[2]};
-    double tri0[3], tri1[3], tri2[3];
-    double t = 0, u = 0, v = 0;
+    const float rayOriginF[3] = {origin[0], origin[1], origin[2]};
+    const float rayDirectionF[3] = {dir[0], dir[1], dir[2]};
     float colour[4] = {0.0f, 0.0f, 0.0f, 255.0f};
     float closest = 300000.0f;
 
     for (int c = 0; c < n_cubes; ++c) { /* :348-377 */
         const float* tris = cube_vertices + 144 * c;
         for (int tri = 0; tri < 36; tri += 3) {
-            for (int k = 0; k < 3; ++k) {
-                tri0[k] = tris[4 * tri + k];
-                tri1[k] = tris[4 * (tri + 1) + k];
-                tri2[k] = tris[4 * (tri + 2) + k];
+            int hit;
+            float tf;
+            if (mode == ORC_CPU) {
+                double tri0[3], tri1[3], tri2[3], t = 0, u = 0, v = 0;
+                for (int k = 0; k < 3; ++k) {
+                    tri0[k] = tris[4 * tri + k];
+                    tri1[k] = tris[4 * (tri + 1) + k];
+                    tri2[k] = tris[4 * (tri + 2) + k];
+                }
+                hit = mt_f64(rayOrigin, rayDirection, tri0, tri1, tri2, &t, &u, &v);
+                tf = (float)t;
+            } else {
+                float tri0[3], tri1[3], tri2[3], t = 0, u = 0, v = 0;
+                for (int k = 0; k < 3; ++k) {
+                    tri0[k] = tris[4 * tri + k];
+                    tri1[k] = tris[4 * (tri + 1) + k];
+                    tri2[k] = tris[4 * (tri + 2) + k];
+                }
+                hit = mt_f32(rayOriginF, rayDirectionF, tri0, tri1, tri2, &t, &u, &v);
+                tf = t;
             }
-            if (orc_intersect_tri(rayOrigin, rayDirection, tri0, tri1, tri2, &t, &u, &v) == 1) {
-                if ((float)t < closest) {
-                    closest = (float)t;
+            if (hit == 1) {
+                if (tf < closest) {
+                    closest = tf;
                     memcpy(colour, cube_colours + 4 * c, sizeof colour);
                 }
             }
         }
     }
     for (int s = 0; s < n_spheres; ++s) { /* :382-394 */
-        float distance = orc_intersect_sphere(origin, dir, sphere_radius[s],
-                                              sphere_origins + 4 * s);
+        float distance = sphere_mode(mode, origin, dir, sphere_radius[s], sphere_origins + 4 * s);
         if (distance == 0.0f) continue;
         if (distance < closest) {
             closest = distance;
@@ -518,19 +589,33 @@ void orc_collide(const float origin[4], const float dir[4], int32_t n_spheres,
     /* :403-406, normaliseFloat(closest, 180, 0) = (closest - 0)/(180 - 0) */
     float normalised = (closest - 0.0f) / (180.0f - 0.0f);
     float colourScalar = 255.0f - (normalised * 255.0f);
-    out[0] = cvt_i32(colourScalar * colour[0]);
-    out[1] = cvt_i32(colourScalar * colour[1]);
-    out[2] = cvt_i32(colourScalar * colour[2]);
+    if (mode == ORC_CL_GFX950) {
+        out[0] = cvt_i32_amdgcn(colourScalar * colour[0]);
+        out[1] = cvt_i32_amdgcn(colourScalar * colour[1]);
+        out[2] = cvt_i32_amdgcn(colourScalar * colour[2]);
+    } else {
+        out[0] = cvt_i32(colourScalar * colour[0]);
+        out[1] = cvt_i32(colourScalar * colour[1]);
+        out[2] = cvt_i32(colourScalar * colour[2]);
+    }
     out[3] = 255;
 }
 
-/* MainState.cpp:936-956 */
-void orc_trace(int32_t width, int32_t height, int32_t row_begin, int32_t row_end,
-               const float ray_dir[4], const float* ray_origins, int32_t n_spheres,
-               const float* sphere_origins, const float* sphere_radius,
-               const float* sphere_colours, int32_t n_cubes, const float* cube_vertices,
-               const float* cube_colours, int32_t* out) {
-    (void)height;
+void orc_collide(const float origin[4], const float dir[4], int32_t n_spheres,
+                 const float* sphere_origins, const float* sphere_radius,
+                 const float* sphere_colours, int32_t n_cubes, const float* cube_vertices,
+                 const float* cube_colours, int32_t out[4]) {
+    collide_mode(ORC_CPU, origin, dir, n_spheres, sphere_origins, sphere_radius, sphere_colours,
+                 n_cubes, cube_vertices, cube_colours, out);
+}
+
+/* MainState.cpp:936-956 (rayTracer.cl's NDRange in the CL modes: one work
+ * item per pixel, origins (x, y, 0, 1) as MainState.cpp:44-50 builds them) */
+static inline __attribute__((always_inline)) void trace_mode(
+    int mode, int32_t width, int32_t row_begin, int32_t row_end, const float ray_dir[4],
+    const float* ray_origins, int32_t n_spheres, const float* sphere_origins,
+    const float* sphere_radius, const float* sphere_colours, int32_t n_cubes,
+    const float* cube_vertices, const float* cube_colours, int32_t* out) {
     for (int32_t y = row_begin; y < row_end; ++y) {
         for (int32_t x = 0; x < width; ++x) {
             float o[4];
@@ -540,11 +625,22 @@ void orc_trace(int32_t width, int32_t height, int32_t row_begin, int32_t row_end
             } else { /* MainState.cpp:44-50 */
                 o[0] = (float)x; o[1] = (float)y; o[2] = 0.0f; o[3] = 1.0f;
             }
-            orc_collide(o, ray_dir, n_spheres, sphere_origins, sphere_radius,
-                        sphere_colours, n_cubes, cube_vertices, cube_colours,
-                        out + 4 * ((int64_t)(y - row_begin) * width + x));
+            collide_mode(mode, o, ray_dir, n_spheres, sphere_origins, sphere_radius,
+                         sphere_colours, n_cubes, cube_vertices, cube_colours,
+                         out + 4 * ((int64_t)(y - row_begin) * width + x));
         }
     }
+}
+
+void orc_trace(int32_t width, int32_t height, int32_t row_begin, int32_t row_end,
+               const float ray_dir[4], const float* ray_origins, int32_t n_spheres,
+               const float* sphere_origins, const float* sphere_radius,
+               const float* sphere_colours, int32_t n_cubes, const float* cube_vertices,
+               const float* cube_colours, int32_t* out) {
+    (void)height;
+    trace_mode(ORC_CPU, width, row_begin, row_end, ray_dir, ray_origins, n_spheres,
+               sphere_origins, sphere_radius, sphere_colours, n_cubes, cube_vertices,
+               cube_colours, out);
 }
 
 typedef struct {
@@ -686,76 +782,28 @@ void orc_pack_rgba8(const int32_t* frame, int64_t n_pixels, uint32_t* out) {
 }
 
 /* ------------------------------------------------------------------------
- * The reference's own OpenCL kernel semantics, rayTracer.cl:37-202, for the
- * record only: its fp32 Moller-Trumbore disagrees with the
- * CPU path on silhouette pixels.  The parity target is orc_trace above; the
- * tests use this to pin the restatement against the survey's probe counts.
+ * The reference's own OpenCL kernel, rayTracer.cl:111-202 (SURVEY.md F5:
+ * its fp32 Moller-Trumbore disagrees with the CPU path on silhouette
+ * pixels).  The parity target is orc_trace; these trace the same
+ * collide_mode text in the kernel's arithmetic:
+ *   orc_trace_cl32        ORC_CL_X86 (the survey probe's host build);
+ *   orc_trace_cl_gfx950   ORC_CL_GFX950 (the kernel compiled for gfx950).
  * ---------------------------------------------------------------------- */
-static int cl_intersect_tri(const float orig[3], const float dir[3], const float vert0[3],
-                            const float vert1[3], const float vert2[3], float* t, float* u,
-                            float* v) {
-    float edge1[3], edge2[3], tvec[3], pvec[3], qvec[3];
-    float det, inv_det;
-    SUB(edge1, vert1, vert0);
-    SUB(edge2, vert2, vert0);
-    CROSS(pvec, dir, edge2);
-    det = DOT(edge1, pvec);
-    if (det > -EPSILON && det < EPSILON) return 0; /* double compare, :54 */
-    inv_det = 1.0 / det;                            /* double literal, :56 */
-    SUB(tvec, orig, vert0);
-    *u = DOT(tvec, pvec) * inv_det;
-    if (*u < 0.0 || *u > 1.0) return 0;
-    CROSS(qvec, tvec, edge1);
-    *v = DOT(dir, qvec) * inv_det;
-    if (*v < 0.0 || *u + *v > 1.0) return 0;
-    *t = DOT(edge2, qvec) * inv_det;
-    return 1;
-}
-
 void orc_trace_cl32(int32_t width, int32_t height, const float ray_dir[4], int32_t n_spheres,
                     const float* sphere_origins, const float* sphere_radius,
                     const float* sphere_colours, int32_t n_cubes, const float* cube_vertices,
                     const float* cube_colours, int32_t* out) {
-    for (int32_t y = 0; y < height; ++y) {
-        for (int32_t x = 0; x < width; ++x) {
-            const float o[4] = {(float)x, (float)y, 0.0f, 1.0f};
-            const float oc[3] = {o[0], o[1], o[2]}, dc[3] = {ray_dir[0], ray_dir[1], ray_dir[2]};
-            float closest = 300000.0f, colour[4] = {0.0f, 0.0f, 0.0f, 255.0f};
-            float t = 0, u = 0, v = 0;
-            for (int c = 0; c < n_cubes; ++c) {
-                for (int tri = 0; tri < 36; tri += 3) {
-                    float a[3], b[3], e[3];
-                    for (int k = 0; k < 3; ++k) {
-                        a[k] = cube_vertices[144 * c + 4 * tri + k];
-                        b[k] = cube_vertices[144 * c + 4 * (tri + 1) + k];
-                        e[k] = cube_vertices[144 * c + 4 * (tri + 2) + k];
-                    }
-                    if (cl_intersect_tri(oc, dc, a, b, e, &t, &u, &v) == 1 && t < closest) {
-                        closest = t;
-                        memcpy(colour, cube_colours + 4 * c, sizeof colour);
-                    }
-                }
-            }
-            for (int s = 0; s < n_spheres; ++s) {
-                float d = orc_intersect_sphere(o, ray_dir, sphere_radius[s], sphere_origins + 4 * s);
-                if (d == 0.0f) continue;
-                if (d < closest) {
-                    closest = d;
-                    memcpy(colour, sphere_colours + 4 * s, sizeof colour);
-                }
-            }
-            int32_t* p = out + 4 * ((int64_t)y * width + x);
-            if (closest == 300000.0f) {
-                p[0] = 0; p[1] = 0; p[2] = 0; p[3] = 255;
-                continue;
-            }
-            float sc = 255.0f - ((closest - 0.0f) / (180.0f - 0.0f)) * 255.0f;
-            p[0] = cvt_i32(sc * colour[0]);
-            p[1] = cvt_i32(sc * colour[1]);
-            p[2] = cvt_i32(sc * colour[2]);
-            p[3] = 255;
-        }
-    }
+    trace_mode(ORC_CL_X86, width, 0, height, ray_dir, NULL, n_spheres, sphere_origins,
+               sphere_radius, sphere_colours, n_cubes, cube_vertices, cube_colours, out);
+}
+
+void orc_trace_cl_gfx950(int32_t width, int32_t height, const float ray_dir[4],
+                         const float* ray_origins, int32_t n_spheres,
+                         const float* sphere_origins, const float* sphere_radius,
+                         const float* sphere_colours, int32_t n_cubes,
+                         const float* cube_vertices, const float* cube_colours, int32_t* out) {
+    trace_mode(ORC_CL_GFX950, width, 0, height, ray_dir, ray_origins, n_spheres, sphere_origins,
+               sphere_radius, sphere_colours, n_cubes, cube_vertices, cube_colours, out);
 }
 
 /* glm::rotate's cos / sin of a float angle (matrix_transform.inl:52-58):

@@ -100,13 +100,23 @@ void orc_trace_rows_mt(int32_t width, int32_t height, const int32_t* rows,
                        const float* cube_vertices, const float* cube_colours,
                        int32_t* out, int32_t n_threads);
 
-/* The reference's fp32 OpenCL kernel semantics (rayTracer.cl:37-202), for
- * the SURVEY.md F5 divergence pin only -- not the parity target. */
+/* The reference's fp32 OpenCL kernel semantics (rayTracer.cl:37-202), the
+ * same collide text as orc_trace in the kernel's arithmetic -- not the
+ * parity target.  cl32: glm dot and x86 (int) (the survey probe's host
+ * build, for the SURVEY.md F5 divergence pin); cl_gfx950: the kernel as
+ * compiled for gfx950 by oracle/Makefile (device-library fma dot,
+ * v_cvt_i32_f32), pinned against that kernel run on the GPU. */
 void orc_trace_cl32(int32_t width, int32_t height, const float ray_dir[4],
                     int32_t n_spheres, const float* sphere_origins,
                     const float* sphere_radius, const float* sphere_colours,
                     int32_t n_cubes, const float* cube_vertices,
                     const float* cube_colours, int32_t* out);
+void orc_trace_cl_gfx950(int32_t width, int32_t height, const float ray_dir[4],
+                         const float* ray_origins, int32_t n_spheres,
+                         const float* sphere_origins, const float* sphere_radius,
+                         const float* sphere_colours, int32_t n_cubes,
+                         const float* cube_vertices, const float* cube_colours,
+                         int32_t* out);
 
 /* Per-pixel hit masks of one triangle (orc_intersect_tri == 1) / one sphere
  * (passes the tca and distance tests) over [x0,x0+w) x [y0,y0+h). */

@@ -53,6 +53,8 @@ def _load() -> ctypes.CDLL:
         "orc_trace_rows_mt": (None, [_i32, _i32, _vp, _i32, _vp, _vp, _i32, _vp, _vp, _vp, _i32,
                                      _vp, _vp, _vp, _i32]),
         "orc_trace_cl32": (None, [_i32, _i32, _vp, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _vp]),
+        "orc_trace_cl_gfx950": (None, [_i32, _i32, _vp, _vp, _i32, _vp, _vp, _vp, _i32, _vp,
+                                       _vp, _vp]),
         "orc_tri_grid": (None, [_vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp]),
         "orc_sphere_grid": (None, [_vp, _f32, _vp, _i32, _i32, _i32, _i32, _vp]),
         "orc_tri_t_grid": (None, [_vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp]),
@@ -149,6 +151,19 @@ class Oracle:
         out = np.zeros((height, width, 4), np.int32)
         self.lib.orc_trace_cl32(width, height, _p(self.ray_dir()), len(sr), _p(so), _p(sr),
                                 _p(sc), len(cc), _p(cv), _p(cc), _p(out))
+        return out
+
+    def trace_cl_gfx950(self, scene, width: int, height: int,
+                        ray_dir: Optional[np.ndarray] = None,
+                        ray_origins: Optional[np.ndarray] = None) -> np.ndarray:
+        """rayTracer.cl's semantics as compiled for gfx950 (the collide text
+        of trace() in the kernel's arithmetic; see rt_oracle.h)."""
+        so, sr, sc, cv, cc = self._arrays(scene)
+        d = self.ray_dir() if ray_dir is None else np.ascontiguousarray(ray_dir, np.float32)
+        org = None if ray_origins is None else np.ascontiguousarray(ray_origins, np.float32)
+        out = np.zeros((height, width, 4), np.int32)
+        self.lib.orc_trace_cl_gfx950(width, height, _p(d), _p(org), len(sr), _p(so), _p(sr),
+                                     _p(sc), len(cc), _p(cv), _p(cc), _p(out))
         return out
 
     def fnv(self, frame: np.ndarray) -> int:

@@ -1,0 +1,104 @@
+"""The oracle pinned against the reference's own OpenCL kernel.
+
+`rayTracer.cl` (resources/shaders/, unmodified) is compiled for gfx950 by
+oracle/Makefile and run on the GPU by tests/ref_kernel.py, with the launch of
+MainState.cpp:841-869 (explicit origins, one work item per pixel).  Its
+frames must equal, bit for bit, the oracle's `orc_trace_cl_gfx950`: the SAME
+collide text as the parity target `orc_trace` (oracle/rt_oracle.c
+`collide_mode`: cubes then spheres in index order, strict `<`, the `t0 == 0`
+skip, the shade and normalise, the frame layout; Moller-Trumbore from one
+source text for both precisions), instantiated with the kernel's arithmetic
+(fp32 triangles, the device library's fma-chained `dot`, v_cvt_i32_f32).
+What the CPU instantiation changes is pinned elsewhere: glm's pairwise dot
+against the reference's vendored glm (test_oracle.py), and the fp64 triangle
+test is the same text as the fp32 one pinned here, in double
+(MainState.cpp:257-298 vs rayTracer.cl:37-78)."""
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+
+from conftest import load_golden
+from ref_kernel import CODE_OBJECT, ReferenceKernel
+from test_gpu_parity import EDGE_CASES, SMALL_FIXTURES, _scene_from, diff_report
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = ("sphere_origins", "sphere_radius", "sphere_colours", "cube_vertices", "cube_colours")
+
+
+@pytest.fixture(scope="module")
+def refk(rt):
+    if not CODE_OBJECT.exists():
+        pytest.skip("oracle/_ref/rayTracer_gfx950.co not built (needs /root/reference)")
+    k = ReferenceKernel()
+    yield k
+    k.close()
+
+
+@pytest.mark.parametrize("name", SMALL_FIXTURES)
+def test_reference_kernel_golden_scenes(refk, oracle, name):
+    """Reference scenes 1-3 (MainState.cpp:419-639) and configs 1-2."""
+    g = load_golden(name)
+    scene = SimpleNamespace(**{k: g[k] for k in FIELDS})
+    w, h = int(g["width"]), int(g["height"])
+    got = refk.trace(scene, w, h, g["ray_dir"])
+    want = oracle.trace_cl_gfx950(scene, w, h, ray_dir=g["ray_dir"])
+    assert not diff_report(got, want), diff_report(got, want)
+    # the kernel is not the parity target: where it differs from the CPU path
+    # (the golden frame) is the fp32-vs-fp64 triangle test and the dot order
+    cpu_diff = int((got != g["frame"]).any(-1).sum())
+    assert cpu_diff < 0.01 * w * h, cpu_diff
+
+
+@pytest.mark.parametrize("case", sorted(EDGE_CASES))
+def test_reference_kernel_edge_cases(pkg, refk, oracle, case):
+    """Ties (first primitive wins), t < 0, t0 == 0, far shades < 0, values
+    > 255, slivers, w != 1, empty scenes."""
+    scene = _scene_from(pkg, **EDGE_CASES[case])
+    d = oracle.ray_dir()
+    got = refk.trace(scene, 101, 77, d)
+    want = oracle.trace_cl_gfx950(scene, 101, 77, ray_dir=d)
+    assert not diff_report(got, want), diff_report(got, want)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_reference_kernel_dense_synthetic(pkg, refk, oracle, seed):
+    """Dense random scenes (the BASELINE generator, overdraw > 1)."""
+    w, h = 320 + 37 * seed, 240 - 11 * seed
+    scene = pkg.Scene.synthetic(w, h, 60 + 20 * seed, 16 + 4 * seed, seed=300 + seed,
+                                k=w / 640 * (2 + seed % 2))
+    d = oracle.ray_dir()
+    got = refk.trace(scene, w, h, d)
+    want = oracle.trace_cl_gfx950(scene, w, h, ray_dir=d)
+    assert not diff_report(got, want), diff_report(got, want)
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_reference_kernel_general_rays(pkg, refk, oracle, seed):
+    """Arbitrary origins and direction (kernel arguments 9-10)."""
+    rng = np.random.default_rng(seed)
+    w, h = 96, 72
+    scene = pkg.Scene.synthetic(w, h, 12, 6, seed=seed, k=0.3)
+    d = np.array([rng.uniform(-0.4, 0.4), rng.uniform(-0.4, 0.4), -1.0, -1.0], np.float32)
+    org = np.zeros((h, w, 4), np.float32)
+    org[..., 0] = np.arange(w)[None, :] + rng.uniform(-0.5, 0.5, (h, w))
+    org[..., 1] = np.arange(h)[:, None] + rng.uniform(-0.5, 0.5, (h, w))
+    org[..., 2] = rng.uniform(-5, 5, (h, w))
+    org[..., 3] = 1.0
+    got = refk.trace(scene, w, h, d, ray_origins=org)
+    want = oracle.trace_cl_gfx950(scene, w, h, ray_dir=d, ray_origins=org)
+    assert not diff_report(got, want), diff_report(got, want)
+
+
+@pytest.mark.parametrize("name", ["scene3_640x480", "config2_1920x1080"])
+def test_reference_kernel_check_sees_the_dot_order(refk, oracle, name):
+    """The comparison is sharp enough to tell the device library's
+    fma-chained dot from glm's pairwise one: with glm's dot (orc_trace_cl32,
+    otherwise the same text) these frames differ from the kernel's."""
+    g = load_golden(name)
+    scene = SimpleNamespace(**{k: g[k] for k in FIELDS})
+    w, h = int(g["width"]), int(g["height"])
+    got = refk.trace(scene, w, h, g["ray_dir"])
+    assert np.array_equal(got, oracle.trace_cl_gfx950(scene, w, h, ray_dir=g["ray_dir"]))
+    assert int((got != oracle.trace_cl32(scene, w, h)).any(-1).sum()) > 0
