@@ -35,6 +35,11 @@ class ReferenceKernel:
         self.hip.hipModuleLoad.argtypes = [ctypes.POINTER(vp), ctypes.c_char_p]
         self.hip.hipModuleGetFunction.argtypes = [ctypes.POINTER(vp), vp, ctypes.c_char_p]
         self.hip.hipModuleUnload.argtypes = [vp]
+        self.hip.hipEventCreate.argtypes = [ctypes.POINTER(vp)]
+        self.hip.hipEventRecord.argtypes = [vp, vp]
+        self.hip.hipEventSynchronize.argtypes = [vp]
+        self.hip.hipEventDestroy.argtypes = [vp]
+        self.hip.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), vp, vp]
         self._check(self.hip.hipSetDevice(device), "hipSetDevice")
         self.module = vp()
         self._check(self.hip.hipModuleLoad(ctypes.byref(self.module), str(path).encode()),
@@ -58,7 +63,10 @@ class ReferenceKernel:
         return p
 
     def trace(self, scene, width: int, height: int, ray_dir: np.ndarray,
-              ray_origins: Optional[np.ndarray] = None) -> np.ndarray:
+              ray_origins: Optional[np.ndarray] = None, timed_reps: int = 0):
+        """The frame (H, W, 4) int32; with timed_reps > 0 also the kernel's
+        milliseconds per launch (HIP events around timed_reps launches on the
+        null stream, after the first), buffers resident."""
         n_px = width * height
         grid = (n_px + self.BLOCK - 1) // self.BLOCK
         padded = grid * self.BLOCK
@@ -85,17 +93,36 @@ class ReferenceKernel:
                     d_cc, d_org, _Float4(*(float(v) for v in d))]
             params = (ctypes.c_void_p * len(vals))(
                 *(ctypes.cast(ctypes.pointer(v), ctypes.c_void_p) for v in vals))
-            self._check(self.hip.hipModuleLaunchKernel(self.fn, grid, 1, 1, self.BLOCK, 1, 1, 0,
-                                                       None, params, None),
-                        "hipModuleLaunchKernel")
+            def launch():
+                self._check(self.hip.hipModuleLaunchKernel(self.fn, grid, 1, 1, self.BLOCK, 1, 1,
+                                                           0, None, params, None),
+                            "hipModuleLaunchKernel")
+            launch()
             self._check(self.hip.hipDeviceSynchronize(), "hipDeviceSynchronize")
+            ms = None
+            if timed_reps > 0:
+                ev = [ctypes.c_void_p(), ctypes.c_void_p()]
+                for e in ev:
+                    self._check(self.hip.hipEventCreate(ctypes.byref(e)), "hipEventCreate")
+                self._check(self.hip.hipEventRecord(ev[0], None), "hipEventRecord")
+                for _ in range(timed_reps):
+                    launch()
+                self._check(self.hip.hipEventRecord(ev[1], None), "hipEventRecord")
+                self._check(self.hip.hipEventSynchronize(ev[1]), "hipEventSynchronize")
+                t = ctypes.c_float()
+                self._check(self.hip.hipEventElapsedTime(ctypes.byref(t), ev[0], ev[1]),
+                            "hipEventElapsedTime")
+                for e in ev:
+                    self.hip.hipEventDestroy(e)
+                ms = t.value / timed_reps
             frame = np.zeros((padded, 4), np.int32)
             self._check(self.hip.hipMemcpy(frame.ctypes.data, out, frame.nbytes, 2),
                         "hipMemcpy D2H")
         finally:
             for p in allocs:
                 self.hip.hipFree(p)
-        return frame[:n_px].reshape(height, width, 4)
+        frame = frame[:n_px].reshape(height, width, 4)
+        return frame if timed_reps <= 0 else (frame, ms)
 
     def close(self):
         if self.module:

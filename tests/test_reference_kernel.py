@@ -102,3 +102,23 @@ def test_reference_kernel_check_sees_the_dot_order(refk, oracle, name):
     got = refk.trace(scene, w, h, g["ray_dir"])
     assert np.array_equal(got, oracle.trace_cl_gfx950(scene, w, h, ray_dir=g["ray_dir"]))
     assert int((got != oracle.trace_cl32(scene, w, h)).any(-1).sum()) > 0
+
+
+def test_reference_kernel_speed_config3(pkg, rt, refk, oracle):
+    """BASELINE config 3 (4096², 256 spheres + 64 cubes, seed 3, k = 6.4)
+    through the reference's own kernel on this GPU -- one work item per
+    pixel, every primitive tested, origins read from HBM -- against the
+    binned HIP path.  Its frame differs from the parity target only on
+    silhouette pixels (fp32 triangles, F5)."""
+    w = h = 4096
+    scene = pkg.Scene.synthetic(w, h, 256, 64, seed=3, k=w / 640)
+    ref_frame, ref_ms = refk.trace(scene, w, h, oracle.ray_dir(), timed_reps=3)
+    frame, _ = rt.render(scene, w, h)
+    ours_ms = min(rt.render(scene, w, h, out=frame)[1].kernel_us for _ in range(5)) / 1e3
+    n_diff = int((frame != ref_frame).any(-1).sum())
+    print(f"\nconfig 3: reference rayTracer.cl on gfx950 {ref_ms:.3f} ms "
+          f"({w * h / ref_ms / 1e3:.0f} Mrays/s); binned HIP path {ours_ms:.4f} ms "
+          f"({w * h / ours_ms / 1e3:.0f} Mrays/s), {ref_ms / ours_ms:.0f}x; "
+          f"{n_diff} of {w * h} pixels differ from the CPU-path frame")
+    assert n_diff < 1e-3 * w * h
+    assert ours_ms * 20 < ref_ms
