@@ -46,6 +46,26 @@ __global__ void __launch_bounds__(64) store_kernel(int4v* out, int width, int n_
             const long long xs = bx4 * 256, ys = by4 * 16 + t;
 #pragma unroll
             for (int j = 0; j < 4; ++j) out[ys * width + xs + j * 64 + lane] = v;
+        } else if (kMode == 7) {
+            const long long bx4 = bin % (n_bx / 4), by4 = bin / (n_bx / 4);
+            const long long xs = bx4 * 256 + 128 * (t % 2), ys = by4 * 16 + 2 * (t / 2);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) out[(ys + j / 2) * width + xs + (j % 2) * 64 + lane] = v;
+        } else if (kMode == 8) {
+            const long long n_by = (long long)gridDim.x / 16 / n_bx;
+            const long long cx = bin / n_by, cy = bin % n_by;
+            const long long xs = cx * 64, ys = cy * 64 + 4 * t;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) out[(ys + j) * width + xs + lane] = v;
+        } else if (kMode == 9) {
+            const long long ys = y0 + (t / 4) + 16 * (t % 4);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) out[(ys + 4 * j) * width + x0 + lane] = v;
+        } else if (kMode == 10) {
+            const long long bx4 = bin % (n_bx / 4), by4 = bin / (n_bx / 4);
+            const long long xs = bx4 * 256 + 64 * (t % 4), ys = by4 * 16 + 4 * (t / 4);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) out[(ys + j) * width + xs + lane] = v;
         } else if (kMode == 4) {
             const long long tx = w % n_bx, ty = w / n_bx;
 #pragma unroll
@@ -92,10 +112,11 @@ int main(int argc, char** argv) {
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
-    const char* names[7] = {"linear 4 KB", "64x4 tiles", "256x1 rows", "16x16 tiles",
-                            "64x4 rowmajor", "16x16 rowmaj", "64x4 via LDS"};
+    const char* names[11] = {"linear 4 KB", "64x4 tiles", "256x1 rows", "16x16 tiles",
+                            "64x4 rowmajor", "16x16 rowmaj", "64x4 via LDS", "128x2 tiles", "64x4 colmajor", "64x4 rows+4",
+                             "64x4 256x16bin"};
     for (int rep = 0; rep < 3; ++rep) {
-        for (int m = 0; m < 7; ++m) {
+        for (int m = 0; m < 11; ++m) {
             auto launch = [&] {
                 if (m == 0) store_kernel<0><<<waves, 64>>>(out, width, n_bx);
                 if (m == 1) store_kernel<1><<<waves, 64>>>(out, width, n_bx);
@@ -104,6 +125,10 @@ int main(int argc, char** argv) {
                 if (m == 4) store_kernel<4><<<waves, 64>>>(out, width, n_bx);
                 if (m == 5) store_kernel<5><<<waves, 64>>>(out, width, n_bx);
                 if (m == 6) store_exchange<<<waves / 4, 256>>>(out, width, n_bx);
+                if (m == 7) store_kernel<7><<<waves, 64>>>(out, width, n_bx);
+                if (m == 8) store_kernel<8><<<waves, 64>>>(out, width, n_bx);
+                if (m == 9) store_kernel<9><<<waves, 64>>>(out, width, n_bx);
+                if (m == 10) store_kernel<10><<<waves, 64>>>(out, width, n_bx);
             };
             launch();
             hipEventRecord(a);
