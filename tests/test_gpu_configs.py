@@ -309,7 +309,8 @@ def test_wide_tile_build_exact(pkg, rt, oracle, case):
         rt.set_tile_variant(0)
 
 
-@pytest.mark.parametrize("seed", list(range(64)))
+# RT_SWEEP_SEEDS widens the sweep for one-off runs (profiles/r02/parity_sweep_4096.log)
+@pytest.mark.parametrize("seed", list(range(int(os.environ.get("RT_SWEEP_SEEDS", "64")))))
 def test_randomized_parity_sweep(pkg, rt, oracle, seed):
     """Seeded random frames against the oracle: frame sizes from 96 to 1500
     px a side, 1 to 600 spheres and 0 to 80 cubes at random densities, row
