@@ -1,5 +1,7 @@
 # A/B of RT_KTOUCH (trace3 touches a batch's record lines before the walk):
 # configs 3, 4 and 5 dense, both formats.
+# (The RT_KTOUCH code was measured and reverted, DESIGN.md §3 rejected table;
+# rebuilding these variants needs it restored from git history.)
 set -u
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out; export TMPDIR=/tmp
 V=opencl-ray-tracer_amd/variants; O=gpurun_out/ab_ktouch.txt; : > $O
