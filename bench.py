@@ -34,7 +34,9 @@ Rank 0 prints ONE JSON line.
 from __future__ import annotations
 
 import argparse
+import datetime
 import json
+import threading
 import os
 import sys
 import time
@@ -94,6 +96,13 @@ def parse(argv=None):
     ap.add_argument("--rehearse", action="store_true",
                     help="N>1 rehearsal on a 1-GPU box: every rank renders on cuda:0 and the "
                          "collectives run over gloo on host copies")
+    ap.add_argument("--pg-timeout", type=float, default=180.0,
+                    help="N>1: seconds before a stuck collective raises / aborts")
+    ap.add_argument("--phase-deadline", type=float, default=120.0,
+                    help="N>1: rank 0 prints the line so far and exits when one measurement "
+                         "phase runs longer than this (below --pg-timeout)")
+    ap.add_argument("--fail-assembly", default="",
+                    help=argparse.SUPPRESS)  # tests: NAME[:RANK] raises in that assembly
     return ap.parse_args(argv)
 
 
@@ -113,28 +122,56 @@ def bytes_to_root(width: int, height: int, world: int, fmt: str, root: int = 0) 
 
 
 def pick_value(assemblies: dict):
-    """The fastest assembly whose frame was bit-exact: (name, entry)."""
+    """The fastest assembly whose frame was bit-exact: (name, entry), or
+    (None, None) when none was (the line then carries value null)."""
     ok = [(v["ms_per_step"], k) for k, v in assemblies.items()
-          if v.get("ms_per_step") is not None and v.get("frame_check") == "bit-exact"]
+          if isinstance(v, dict) and v.get("ms_per_step") is not None
+          and v.get("frame_check") == "bit-exact"]
     if not ok:
-        raise RuntimeError(f"no assembly produced a bit-exact frame: {assemblies}")
+        return None, None
     ms, name = min(ok)
     return name, assemblies[name]
 
 
+def cpu_quota(root: str = "/sys/fs/cgroup"):
+    """The job's CPU quota from its cgroup, in CPUs, and the file it came
+    from: cgroup v2 `cpu.max` ("quota period" or "max ..."), else v1
+    `cpu/cpu.cfs_quota_us` / `cpu.cfs_period_us` (-1 = none).  (None, path)
+    when no quota is set, (None, None) when neither file exists."""
+    v2 = Path(root) / "cpu.max"
+    try:
+        q, per = v2.read_text().split()[:2]
+        return (None if q == "max" else int(q) / int(per)), str(v2)
+    except (OSError, ValueError):
+        pass
+    v1 = Path(root) / "cpu" / "cpu.cfs_quota_us"
+    try:
+        q = int(v1.read_text())
+        per = int((Path(root) / "cpu" / "cpu.cfs_period_us").read_text())
+        return (None if q <= 0 or per <= 0 else q / per), str(v1)
+    except (OSError, ValueError):
+        return None, None
+
+
 def cpu_threads(requested: int) -> tuple:
     """(threads to use, description).  0 = every CPU this job may run on:
-    the affinity set, capped by the job's CPU share where the launcher
-    states one (OMP_NUM_THREADS; the GPU box grants 16 CPUs per GPU)."""
+    the affinity set, capped by the job's CPU share -- its cgroup CPU quota,
+    and the launcher's OMP_NUM_THREADS where it states one (the GPU box
+    grants 16 CPUs per GPU)."""
     affinity = len(os.sched_getaffinity(0))
     share = os.environ.get("OMP_NUM_THREADS")
+    quota, quota_src = cpu_quota()
     n = affinity
+    if quota is not None:
+        n = min(n, max(1, int(quota)))
     if share and share.isdigit() and int(share) > 0:
         n = min(n, int(share))
     if requested > 0:
         n = min(requested, affinity)
     return max(1, n), {"affinity_cpus": affinity, "os_cpu_count": os.cpu_count(),
-                       "omp_num_threads": share}
+                       "omp_num_threads": share,
+                       "cgroup_cpu_quota": None if quota is None else round(quota, 2),
+                       "cgroup_quota_file": quota_src}
 
 
 class Ctx:
@@ -156,10 +193,15 @@ class Ctx:
         if self.distributed:
             os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
             torch.cuda.set_device(self.gpu)
+            # a stuck collective raises (gloo) or aborts (RCCL) after this
+            # long instead of blocking the run; rank 0's phase watchdog
+            # (Phases) prints the line before it
+            timeout = datetime.timedelta(seconds=args.pg_timeout)
             if self.backend == "nccl":
-                dist.init_process_group("nccl", device_id=torch.device("cuda", self.gpu))
+                dist.init_process_group("nccl", device_id=torch.device("cuda", self.gpu),
+                                        timeout=timeout)
             else:
-                dist.init_process_group("gloo")
+                dist.init_process_group("gloo", timeout=timeout)
         self.dev = torch.device("cuda", self.gpu)
         # collectives move GPU tensors with RCCL, host copies with gloo
         self.coll_dev = self.dev if self.backend == "nccl" else torch.device("cpu")
@@ -214,6 +256,90 @@ class Ctx:
         wall = (time.perf_counter() - t0) * 1e3 / steps
         self.barrier()
         return self.max_over_ranks(wall)
+
+
+class Phases:
+    """The N>1 run as named phases, so one failing or hanging measurement
+    never costs the JSON line (rank 0 prints it in every case).
+
+    run(key, fn): fn() on every rank; its value goes to target[key].  An
+    exception on any rank becomes {"error": ...} under that key on every
+    rank: the ranks agree over a separate gloo group (`ctrl`), so the
+    agreement never pairs with a data-path collective another rank is still
+    blocked in (that rank's collective times out after --pg-timeout and it
+    joins the agreement).  A phase still running after `deadline_s` makes
+    rank 0's watchdog print the line built so far, that phase marked
+    {"error": "timeout ..."}, and end the process (os._exit(0)): the driver
+    still gets its line when an RCCL collective hangs (RCCL would abort the
+    process only later, at --pg-timeout)."""
+
+    def __init__(self, c, deadline_s: float, finish, pg_timeout_s: float = 180.0):
+        self.c = c
+        self.deadline = deadline_s
+        self.finish = finish  # () -> the line dict to print (rank 0)
+        self.current = None   # (key, target dict, start time)
+        self.printed = False
+        self.lock = threading.Lock()
+        self.ctrl = None
+        if c.distributed:
+            # longer than the data-path timeout: a rank that failed early
+            # waits here while the others' collective of that phase times out
+            self.ctrl = c.dist.new_group(
+                backend="gloo", timeout=datetime.timedelta(seconds=3 * pg_timeout_s + 60))
+        if c.rank == 0:
+            threading.Thread(target=self._watch, daemon=True).start()
+
+    def _watch(self):
+        while True:
+            time.sleep(0.5)
+            with self.lock:
+                cur = self.current
+                if cur is None or self.printed:
+                    continue
+                key, target, t0 = cur
+                if time.monotonic() - t0 < self.deadline:
+                    continue
+                target[key] = {"error": f"timeout: phase still running after "
+                                        f"{self.deadline:.0f} s (rank 0's watchdog)"}
+                self.emit()
+            sys.stdout.flush()
+            os._exit(0)
+
+    def emit(self):
+        """Print the line once (rank 0)."""
+        if self.c.rank == 0 and not self.printed:
+            self.printed = True
+            print(json.dumps(self.finish()), flush=True)
+
+    def agree(self, ok: bool) -> bool:
+        if self.ctrl is None:
+            return ok
+        t = self.c.torch.tensor([1 if ok else 0], dtype=self.c.torch.int32)
+        self.c.dist.all_reduce(t, op=self.c.dist.ReduceOp.MIN, group=self.ctrl)
+        return bool(int(t.item()))
+
+    def run(self, key: str, fn, target: dict):
+        with self.lock:
+            self.current = (key, target, time.monotonic())
+        err = None
+        try:
+            val = fn()
+        except Exception as e:  # recorded; the other phases still run
+            val, err = None, f"rank {self.c.rank}: {type(e).__name__}: {e}"
+        ok = self.agree(err is None)
+        with self.lock:
+            self.current = None
+            target[key] = val if ok else {"error": err or "failed on another rank"}
+        return target[key]
+
+
+def failing(args, c, name: str) -> bool:
+    """--fail-assembly NAME[:RANK] (tests): does assembly NAME raise on this
+    rank?"""
+    if not args.fail_assembly:
+        return False
+    what, _, rank = args.fail_assembly.partition(":")
+    return what == name and (rank == "" or int(rank) == c.rank)
 
 
 def device_scene(pkg, c: Ctx, width, height, spheres, cubes, seed, k):
@@ -423,16 +549,44 @@ def cpu_baseline(args, scene, w, h):
     c1 = time.perf_counter()
     orc.trace_rows(scene, w, h, serial_rows, threads=1)
     s_s = time.perf_counter() - c1
-    return {"value": round(len(sample_rows) * w / c_s / 1e6, 3), "unit": "Mrays/s",
-            "cores": threads, "kind": "port",
-            "host_cpus": cpus,
-            "sample": (f"the whole {w}x{len(sample_rows)} frame" if args.cpu_rows == 1 else
-                       f"{len(sample_rows)} rows (every {args.cpu_rows}th) x {w} px")
-                      + f" of the same scene, oracle/rt_oracle.c orc_trace_rows_mt on "
-                        f"{threads} threads (one row band per thread), {c_s:.1f} s wall",
-            "serial_1core": {"value": round(len(serial_rows) * w / s_s / 1e6, 3),
-                             "sample": f"every 32nd row ({len(serial_rows)} rows x {w} px), "
-                                       f"1 thread, {s_s:.1f} s wall"}}
+    res = {"value": round(len(sample_rows) * w / c_s / 1e6, 3), "unit": "Mrays/s",
+           "cores": threads, "kind": "port",
+           "cores_scope": "the job's CPU share: the affinity set capped by the cgroup quota "
+                          "and OMP_NUM_THREADS (host_cpus)",
+           "host_cpus": cpus,
+           "sample": (f"the whole {w}x{len(sample_rows)} frame" if args.cpu_rows == 1 else
+                      f"{len(sample_rows)} rows (every {args.cpu_rows}th) x {w} px")
+                     + f" of the same scene, oracle/rt_oracle.c orc_trace_rows_mt on "
+                       f"{threads} threads (one row band per thread), {c_s:.1f} s wall",
+           "serial_1core": {"value": round(len(serial_rows) * w / s_s / 1e6, 3),
+                            "sample": f"every 32nd row ({len(serial_rows)} rows x {w} px), "
+                                      f"1 thread, {s_s:.1f} s wall"}}
+    # SURVEY.md §8d (b) asks for all host cores: when no cgroup quota caps the
+    # job below its affinity set, a second leg on every CPU of the affinity
+    # set (a sample of rows, so it stays short); `cores` stays the first leg
+    aff = cpus["affinity_cpus"]
+    quota = cpus["cgroup_cpu_quota"]
+    share = cpus["omp_num_threads"]
+    capped = (quota is not None and quota < aff) or (
+        share is not None and share.isdigit() and 0 < int(share) < aff)
+    if args.cpu_threads == 0 and aff > threads and not capped:
+        step = max(1, args.cpu_rows, h * aff // (threads * 4096) if threads else 1)
+        rows_all = list(range(0, h, step))
+        c2 = time.perf_counter()
+        orc.trace_rows(scene, w, h, rows_all, threads=aff)
+        a_s = time.perf_counter() - c2
+        res["all_affinity_cpus"] = {
+            "value": round(len(rows_all) * w / a_s / 1e6, 3), "cores": aff,
+            "sample": f"every {step}th row ({len(rows_all)} rows x {w} px), {aff} threads, "
+                      f"{a_s:.1f} s wall"}
+    else:
+        res["all_affinity_cpus"] = None
+        res["all_affinity_cpus_skipped"] = (
+            "the first leg already uses every CPU of the affinity set" if aff <= threads else
+            f"the cgroup quota ({quota} CPUs) or the launcher's share "
+            f"(OMP_NUM_THREADS={cpus['omp_num_threads']}) caps this job at {threads} of the "
+            f"{aff} CPUs in its affinity set")
+    return res
 
 
 # ---------------------------------------------------------------------------
@@ -550,7 +704,10 @@ def _wrap_device(c: Ctx, ptr: int, rows, width, fmt):
     return torch.as_tensor(_Arr(), device=c.dev)
 
 
-def measure_assembly(args, c, pkg, rt, ds, width, height, fmt, how, split=False, bands=None):
+def measure_assembly(args, c, pkg, rt, ds, width, height, fmt, how, split=False, bands=None,
+                     name=None):
+    if failing(args, c, name or how):
+        raise RuntimeError(f"--fail-assembly {args.fail_assembly}")
     a = Assembly(c, pkg, rt, ds, width, height, fmt, how, bands=bands)
     if a.error:
         a.close()  # frees what the root allocated; a barrier on every rank
@@ -587,15 +744,19 @@ def calibrate_peer_store(args, c, pkg, rt, ds, width, height, fmt):
     from opencl_ray_tracer_amd import rowbands
 
     row_bytes = width * BYTES_PER_RAY[fmt]
+    # two band sizes of at least 16 rows per rank must fit the frame (the
+    # same decision on every rank, so no rank is left in a collective)
+    if height < 2 * 16 * c.world:
+        return None
     shared = rowbands.SharedFrame(rt, row_bytes * height, row_bytes, c.rank,
                                   handle_device=c.coll_dev)
     try:
         if not shared.ok:
             return None
         times = []
-        sizes = [max(16, height // c.world), max(16, height // (2 * c.world))]
+        sizes = [height // c.world, max(16, height // (2 * c.world))]
         for n in sizes:
-            rb = c.rank * n
+            rb = c.rank * n  # rb + n <= height: n <= height // world
             step = rt.bind_render_device(ds, width, height, (rb, rb + n), shared.ptr_of_row(rb),
                                          fmt=fmt, stream=c.stream.cuda_stream)
             for _ in range(args.warmup):
@@ -695,136 +856,194 @@ def device_scene_from(c: Ctx, scene):
     return t, ds
 
 
-def measure_assemblies(args, c, pkg, rt, ds, w, h, fmt, split=False):
+def measure_assemblies(args, c, pkg, rt, ds, w, h, fmt, phases, res, split=False):
     """The frame assembled on rank 0 three ways: equal bands by RCCL
     point-to-point, equal bands by xGMI peer stores, and cost-balanced bands
     by xGMI peer stores.  The equal split makes every other rank wait on its
     link while rank 0's own rows need no transfer, so the balanced split
     sizes the bands by each rank's measured cost (render + stores into rank
     0's frame) for all ranks to finish together (rowbands.balanced_bands).
-    Same frame, same end point, each checked bit-exactly."""
+    Same frame, same end point, each checked bit-exactly.  Each assembly is
+    its own phase: one that raises or hangs is recorded as {"error": ...}
+    in `res` and the others still run."""
     from opencl_ray_tracer_amd import rowbands
 
-    res = {how: measure_assembly(args, c, pkg, rt, ds, w, h, fmt, how, split=split)
-           for how in ("rccl_p2p", "xgmi_peer_store")}
-    costs = calibrate_peer_store(args, c, pkg, rt, ds, w, h, fmt)
-    if costs is not None:
+    for how in ("rccl_p2p", "xgmi_peer_store"):
+        phases.run(how, lambda how=how: measure_assembly(args, c, pkg, rt, ds, w, h, fmt, how,
+                                                         split=split), res)
+
+    def balanced():
+        costs = calibrate_peer_store(args, c, pkg, rt, ds, w, h, fmt)
+        if costs is None:
+            return {"ms_per_step": None, "error": "no calibration (frame too short or no "
+                                                  "shared mapping)"}
         bal = rowbands.balanced_bands(h, costs)
-        res["xgmi_peer_store_balanced"] = measure_assembly(
-            args, c, pkg, rt, ds, w, h, fmt, "xgmi_peer_store", split=split, bands=bal)
-        res["xgmi_peer_store_balanced"]["cost_model_us"] = [
-            {"fixed": round(a * 1e6, 2), "per_row": round(s * 1e6, 4)} for a, s in costs]
+        r = measure_assembly(args, c, pkg, rt, ds, w, h, fmt, "xgmi_peer_store", split=split,
+                             bands=bal, name="xgmi_peer_store_balanced")
+        r["cost_model_us"] = [{"fixed": round(a * 1e6, 2), "per_row": round(s * 1e6, 4)}
+                              for a, s in costs]
+        return r
+    phases.run("xgmi_peer_store_balanced", balanced, res)
     return res
 
 
-def run_multi(args, c: Ctx, pkg):
-    from opencl_ray_tracer_amd import rowbands
-
+def multi_line(args, c: Ctx, state: dict) -> dict:
+    """The N>1 JSON line from the phases that have finished (`state`); a
+    phase that failed or timed out appears as {"error": ...}."""
     w, h = args.width, args.height
     k = args.k if args.k is not None else w / 640.0
-    scene, ds = device_scene(pkg, c, w, h, args.spheres, args.cubes, args.seed, k)
-    rt = pkg.RayTracer(c.gpu)
-    rb, re = rowbands.band_rows(h, c.world, c.rank)
-    # untimed: bring every GPU to its steady clock (renders of this rank's band)
-    ramp_out = frame_tensor(c, max(re - rb, 1), w, args.format)
-    ramp = (rt.bind_render_device(ds, w, h, (rb, re), ramp_out.data_ptr(), fmt=args.format,
-                                  stream=c.stream.cuda_stream) if re > rb else (lambda: None))
-    ramp_steps = c.clock_ramp(ramp, args.warmup_ms)
-    del ramp_out
-
-    assemblies = measure_assemblies(args, c, pkg, rt, ds, w, h, args.format, split=True)
-    best, entry = pick_value(assemblies)
-    ms = entry["ms_per_step"]
-
-    # the trace kernel on this rank's band, local stores (the roofline of the
-    # dominant kernel; rank 0's band)
-    band = frame_tensor(c, max(re - rb, 1), w, args.format)
-    step = (rt.bind_render_device(ds, w, h, (rb, re), band.data_ptr(), fmt=args.format,
-                                  stream=c.stream.cuda_stream) if re > rb else (lambda: None))
-    for _ in range(args.warmup):
-        step()
-    rt.profile(True)
-    for _ in range(args.steps):
-        step()
-    prof = rt.profile_read()
-    rt.profile(False)
-    n = max(prof["renders"], 1)
-    trace_ms = prof["trace_ms"] / n
-    band_bytes = BYTES_PER_RAY[args.format] * w * (re - rb)
-    achieved = band_bytes / (trace_ms * 1e-3) / 1e9 if trace_ms > 0 else 0.0
-    del band
-
-    extras = {}
-    if not args.no_extras:
-        # the Texture (RGBA8, MainState.cpp:1023-1037) assembled the same way
-        extras["texture_rgba8"] = measure_assemblies(args, c, pkg, rt, ds, w, h, "rgba8")
-        # BASELINE config 4: 8192^2, 192 + 64, row-tiled with the assembly
-        c4 = CONFIG4
-        k4 = c4["width"] / 640.0
-        _, ds4 = device_scene(pkg, c, c4["width"], c4["height"], c4["spheres"], c4["cubes"],
-                              c4["seed"], k4)
-        extras["config4"] = {
-            "workload": f"config4: {c4['width']}x{c4['height']} frame, {c4['spheres']} spheres + "
-                        f"{c4['cubes']} cubes, dense k={k4:.1f}, seed {c4['seed']}, "
-                        f"{c.world} row bands (BASELINE names 8 GPUs)",
-            **measure_assemblies(args, c, pkg, rt, ds4, c4["width"], c4["height"], "i32x4")}
-        del ds4
-        # weak scaling (secondary): a 4096 x 4096N frame with N x (256 + 64)
-        # primitives of the same density, rank r renders rows [4096 r, 4096 (r+1))
-        hw = h * c.world
-        _, dsw = device_scene(pkg, c, w, hw, args.spheres * c.world, args.cubes * c.world,
-                              args.seed, k)
-        outw = frame_tensor(c, h, w, args.format)
-        stepw = rt.bind_render_device(dsw, w, hw, (c.rank * h, (c.rank + 1) * h),
-                                      outw.data_ptr(), fmt=args.format,
-                                      stream=c.stream.cuda_stream)
-        for _ in range(args.warmup):
-            stepw()
-        wms = c.timed(stepw, args.steps)
-        extras["weak_scaling"] = {
-            "workload": f"{w}x{hw} frame, {args.spheres * c.world} spheres + "
-                        f"{args.cubes * c.world} cubes; each rank renders {w}x{h} rows, "
-                        f"no assembly",
-            "ms_per_step": round(wms, 4), "mrays": round(mrays_per_s(w * hw, wms), 1)}
-        del outw, dsw
-        # the app's host frame filled by every GPU over its own PCIe link
-        extras["host_frame"] = measure_host_frame(args, c, pkg, rt, scene, w, h)
-
-    rt.close()
+    asm = state.get("assembly", {})
+    best, entry = pick_value(asm)
+    ms = entry["ms_per_step"] if entry else None
     workload = CONFIG_NAMES.get((w, h, args.spheres, args.cubes), "custom")
-    return {
-        "metric": METRIC, "value": round(mrays_per_s(w * h, ms), 1), "unit": "Mrays/s",
-        "n_gpus": c.world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "strong",
-        "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+    line = {
+        "metric": METRIC, "value": round(mrays_per_s(w * h, ms), 1) if ms else None,
+        "unit": "Mrays/s", "n_gpus": c.world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(ms, 4) if ms else None, "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
         "config": {"workload": f"{workload}: {w}x{h} frame, {args.spheres} spheres + "
                                f"{args.cubes} cubes, dense k={k:.2f}, seed {args.seed}",
                    "width": w, "height": h, "spheres": args.spheres, "cubes": args.cubes,
                    "format": args.format,
-                   "parallelism": f"row-bands x{c.world}, frame assembled on rank 0 by {best}"
+                   "parallelism": f"row-bands x{c.world}, frame assembled on rank 0 by "
+                                  f"{best or 'none (no bit-exact assembly)'}"
                                   + (" (rehearsal: shared cuda:0, gloo)" if args.rehearse
                                      else "")},
-        "assembly": assemblies,
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                     "kernel": "trace3_kernel", "kernel_ms": round(trace_ms, 4),
-                     "algo_bytes_per_launch": band_bytes,
-                     "scope": "rank 0's band, local stores"},
-        **extras,
-        "clock_ramp": {"ms": args.warmup_ms, "untimed_steps": ramp_steps},
-        "cpu_baseline": None,
+        "assembly": asm,
+        "roofline": state.get("roofline"),
     }
+    for key in ("texture_rgba8", "config4", "weak_scaling", "host_frame"):
+        if key in state:
+            line[key] = state[key]
+    line["clock_ramp"] = (state.get("setup") or {}).get("clock_ramp")
+    line["cpu_baseline"] = state.get("cpu_baseline")
+    errors = sorted(f"{key}.{sub}" if sub else key
+                    for key, v in state.items() if isinstance(v, dict)
+                    for sub in ([None] if "error" in v else
+                                [s for s, e in v.items() if isinstance(e, dict) and "error" in e]))
+    if errors:
+        line["phase_errors"] = errors
+    return line
+
+
+def run_multi(args, c: Ctx, pkg):
+    """N>1: every measurement is a phase (Phases), so the line is printed on
+    rank 0 whatever one of them does."""
+    from opencl_ray_tracer_amd import rowbands
+
+    w, h = args.width, args.height
+    k = args.k if args.k is not None else w / 640.0
+    state = {"assembly": {}}
+    env = {}
+    phases = Phases(c, args.phase_deadline, lambda: multi_line(args, c, state), args.pg_timeout)
+    rb, re = rowbands.band_rows(h, c.world, c.rank)
+
+    def setup():
+        env["scene"], env["ds"] = device_scene(pkg, c, w, h, args.spheres, args.cubes,
+                                               args.seed, k)
+        env["rt"] = rt = pkg.RayTracer(c.gpu)
+        # untimed: bring every GPU to its steady clock (renders of this rank's band)
+        ramp_out = frame_tensor(c, max(re - rb, 1), w, args.format)
+        ramp = (rt.bind_render_device(env["ds"], w, h, (rb, re), ramp_out.data_ptr(),
+                                      fmt=args.format, stream=c.stream.cuda_stream)
+                if re > rb else (lambda: None))
+        steps = c.clock_ramp(ramp, args.warmup_ms)
+        c.sync()
+        return {"clock_ramp": {"ms": args.warmup_ms, "untimed_steps": steps}}
+    phases.run("setup", setup, state)
+    if "error" in state["setup"]:
+        phases.emit()
+        return
+    rt, ds, scene = env["rt"], env["ds"], env["scene"]
+
+    measure_assemblies(args, c, pkg, rt, ds, w, h, args.format, phases, state["assembly"],
+                       split=True)
+
+    def roofline():
+        # the trace kernel on this rank's band, local stores (the roofline of
+        # the dominant kernel; rank 0's band)
+        band = frame_tensor(c, max(re - rb, 1), w, args.format)
+        step = (rt.bind_render_device(ds, w, h, (rb, re), band.data_ptr(), fmt=args.format,
+                                      stream=c.stream.cuda_stream) if re > rb else (lambda: None))
+        for _ in range(args.warmup):
+            step()
+        rt.profile(True)
+        for _ in range(args.steps):
+            step()
+        prof = rt.profile_read()
+        rt.profile(False)
+        trace_ms = prof["trace_ms"] / max(prof["renders"], 1)
+        band_bytes = BYTES_PER_RAY[args.format] * w * (re - rb)
+        achieved = band_bytes / (trace_ms * 1e-3) / 1e9 if trace_ms > 0 else 0.0
+        return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "kernel": kernel_name(args), "kernel_ms": round(trace_ms, 4),
+                "algo_bytes_per_launch": band_bytes, "scope": "rank 0's band, local stores"}
+    phases.run("roofline", roofline, state)
+
+    if not args.no_extras:
+        # the Texture (RGBA8, MainState.cpp:1023-1037) assembled the same way
+        state["texture_rgba8"] = {}
+        measure_assemblies(args, c, pkg, rt, ds, w, h, "rgba8", phases, state["texture_rgba8"])
+        # BASELINE config 4: 8192^2, 192 + 64, row-tiled with the assembly
+        c4 = CONFIG4
+        k4 = c4["width"] / 640.0
+        state["config4"] = {
+            "workload": f"config4: {c4['width']}x{c4['height']} frame, {c4['spheres']} "
+                        f"spheres + {c4['cubes']} cubes, dense k={k4:.1f}, seed {c4['seed']}, "
+                        f"{c.world} row bands (BASELINE names 8 GPUs)"}
+
+        def scene4():
+            env["ds4"] = device_scene(pkg, c, c4["width"], c4["height"], c4["spheres"],
+                                      c4["cubes"], c4["seed"], k4)[1]
+            return "ok"
+        if phases.run("scene", scene4, state["config4"]) == "ok":
+            del state["config4"]["scene"]
+            measure_assemblies(args, c, pkg, rt, env.pop("ds4"), c4["width"], c4["height"],
+                               "i32x4", phases, state["config4"])
+
+        def weak():
+            # weak scaling (secondary): a 4096 x 4096N frame with N x (256 +
+            # 64) primitives of the same density; rank r renders rows
+            # [4096 r, 4096 (r + 1))
+            hw = h * c.world
+            _, dsw = device_scene(pkg, c, w, hw, args.spheres * c.world, args.cubes * c.world,
+                                  args.seed, k)
+            outw = frame_tensor(c, h, w, args.format)
+            stepw = rt.bind_render_device(dsw, w, hw, (c.rank * h, (c.rank + 1) * h),
+                                          outw.data_ptr(), fmt=args.format,
+                                          stream=c.stream.cuda_stream)
+            for _ in range(args.warmup):
+                stepw()
+            wms = c.timed(stepw, args.steps)
+            return {"workload": f"{w}x{hw} frame, {args.spheres * c.world} spheres + "
+                                f"{args.cubes * c.world} cubes; each rank renders {w}x{h} "
+                                f"rows, no assembly",
+                    "ms_per_step": round(wms, 4), "mrays": round(mrays_per_s(w * hw, wms), 1)}
+        phases.run("weak_scaling", weak, state)
+        # the app's host frame filled by every GPU over its own PCIe link
+        phases.run("host_frame", lambda: measure_host_frame(args, c, pkg, rt, scene, w, h),
+                   state)
+
+    # the CPU path beside the GPU numbers (SURVEY.md §8d), timed on rank 0's
+    # host CPUs while the other ranks wait
+    if not args.no_cpu_baseline:
+        phases.run("cpu_baseline",
+                   lambda: cpu_baseline(args, scene, w, h) if c.rank == 0 else None, state)
+    rt.close()
+    phases.emit()
 
 
 def main():
     args = parse()
     c = Ctx(args)
     pkg = __graft_entry__.load_package()
-    line = run_multi(args, c, pkg) if c.distributed else run_single(args, c, pkg)
-    if c.rank == 0:
-        print(json.dumps(line), flush=True)
     if c.distributed:
+        run_multi(args, c, pkg)  # rank 0 prints the line
         c.dist.destroy_process_group()
+        return
+    line = run_single(args, c, pkg)
+    print(json.dumps(line), flush=True)
 
 
 if __name__ == "__main__":

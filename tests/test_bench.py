@@ -48,8 +48,25 @@ def test_bench_arithmetic():
     asm["xgmi_peer_store"]["frame_check"] = "MISMATCH"
     assert b.pick_value(asm)[0] == "rccl_p2p"
     asm["rccl_p2p"] = {"ms_per_step": None, "error": "no mapping"}
-    with pytest.raises(RuntimeError):
-        b.pick_value(asm)
+    assert b.pick_value(asm) == (None, None)  # the line then carries value null
+    asm["rccl_p2p"] = {"error": "rank 1: RuntimeError: boom"}  # a failed phase
+    assert b.pick_value(asm) == (None, None)
+
+
+def test_cpu_quota(tmp_path):
+    b = _bench()
+    assert b.cpu_quota(str(tmp_path)) == (None, None)  # no cgroup files
+    (tmp_path / "cpu.max").write_text("max 100000\n")
+    assert b.cpu_quota(str(tmp_path)) == (None, str(tmp_path / "cpu.max"))
+    (tmp_path / "cpu.max").write_text("1600000 100000\n")
+    assert b.cpu_quota(str(tmp_path))[0] == 16.0
+    (tmp_path / "cpu.max").unlink()
+    (tmp_path / "cpu").mkdir()
+    (tmp_path / "cpu" / "cpu.cfs_quota_us").write_text("-1\n")
+    (tmp_path / "cpu" / "cpu.cfs_period_us").write_text("100000\n")
+    assert b.cpu_quota(str(tmp_path))[0] is None
+    (tmp_path / "cpu" / "cpu.cfs_quota_us").write_text("800000\n")
+    assert b.cpu_quota(str(tmp_path))[0] == 8.0
 
 
 def test_cpu_threads_report(monkeypatch):
@@ -60,8 +77,10 @@ def test_cpu_threads_report(monkeypatch):
     assert n == min(3, aff)
     assert info["affinity_cpus"] == aff and info["os_cpu_count"] == os.cpu_count()
     monkeypatch.delenv("OMP_NUM_THREADS")
-    assert b.cpu_threads(0)[0] == aff
+    quota = b.cpu_quota()[0]
+    assert b.cpu_threads(0)[0] == (aff if quota is None else min(aff, max(1, int(quota))))
     assert b.cpu_threads(1)[0] == 1
+    assert "cgroup_cpu_quota" in b.cpu_threads(0)[1]
 
 
 def test_bench_parse_defaults():
@@ -181,3 +200,134 @@ def test_balanced_bands():
     assert [e - s for s, e in b] == [100, 0]
     with pytest.raises(ValueError):
         balanced_bands(10, [(0.0, 0.0)])
+
+
+class _FakeCtx:
+    """bench.Ctx's collective plumbing on gloo, without a GPU."""
+
+    def __init__(self, rank, world):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist = torch, dist
+        self.rank, self.world = rank, world
+        self.distributed = world > 1
+        self.coll_dev = torch.device("cpu")
+
+
+def _args(b, extra=()):
+    return b.parse(["--gpus", "2", *extra])
+
+
+def _phases_worker(rank, world, port, out_path):
+    """Two gloo ranks run the N>1 line's phases with failures forced in
+    them: an assembly raising on every rank, one raising on rank 1 only while
+    rank 0 waits in a collective of that phase (it times out and joins the
+    agreement), an extra phase that fails; rank 0 writes the printed line."""
+    import datetime
+    import io
+    import contextlib
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, str(REPO))
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=5))
+    try:
+        b = _bench()
+        c = _FakeCtx(rank, world)
+        args = _args(b, ["--fail-assembly", "xgmi_peer_store"])
+        state = {"assembly": {}}
+        buf = io.StringIO()
+        with contextlib.redirect_stdout(buf):
+            ph = b.Phases(c, 60.0, lambda: b.multi_line(args, c, state), pg_timeout_s=20.0)
+
+            def ok_assembly():
+                dist.barrier()
+                return {"ms_per_step": 0.5, "frame_check": "bit-exact"}
+
+            def forced():
+                if b.failing(args, c, "xgmi_peer_store"):
+                    raise RuntimeError(f"--fail-assembly {args.fail_assembly}")
+                return {"ms_per_step": 0.1, "frame_check": "bit-exact"}
+
+            def one_rank():
+                if rank == 1:
+                    raise RuntimeError("rank 1 only")
+                dist.barrier()  # rank 0 blocks here until the gloo timeout
+                return {"ms_per_step": 0.05, "frame_check": "bit-exact"}
+
+            ph.run("rccl_p2p", ok_assembly, state["assembly"])
+            ph.run("xgmi_peer_store", forced, state["assembly"])
+            ph.run("xgmi_peer_store_balanced", one_rank, state["assembly"])
+            ph.run("weak_scaling", lambda: 1 / 0, state)
+            ph.run("roofline", lambda: {"frac": 0.5}, state)
+            ph.emit()
+        if rank == 0:
+            with open(out_path, "w") as f:
+                f.write(buf.getvalue())
+        else:
+            assert buf.getvalue() == ""  # only rank 0 prints
+    finally:
+        dist.destroy_process_group()
+
+
+def test_phases_record_failures_gloo(tmp_path):
+    """N>1 bench: an assembly that raises (on every rank, or on one rank while
+    the other waits in a collective) is recorded as {"error": ...}, the other
+    phases still run, and rank 0 prints ONE line that parses."""
+    import json
+    import torch.multiprocessing as mp
+
+    out = tmp_path / "line.txt"
+    mp.spawn(_phases_worker, args=(2, _free_port(), str(out)), nprocs=2, join=True)
+    lines = [l for l in out.read_text().splitlines() if l.strip()]
+    assert len(lines) == 1
+    line = json.loads(lines[0])
+    asm = line["assembly"]
+    assert "error" in asm["xgmi_peer_store"] and "--fail-assembly" in asm["xgmi_peer_store"]["error"]
+    assert "error" in asm["xgmi_peer_store_balanced"]
+    assert asm["rccl_p2p"]["frame_check"] == "bit-exact"
+    # value from the one assembly that completed bit-exactly
+    assert line["ms_per_step"] == 0.5 and line["value"] == pytest.approx(4096 * 4096 / 0.5e-3 / 1e6, rel=1e-3)
+    assert "error" in line["weak_scaling"] and line["roofline"] == {"frac": 0.5}
+    assert line["phase_errors"] == ["assembly.xgmi_peer_store",
+                                    "assembly.xgmi_peer_store_balanced", "weak_scaling"]
+    assert line["n_gpus"] == 2 and line["metric"]
+
+
+_WATCHDOG = r"""
+import sys, time
+sys.path.insert(0, {repo!r})
+sys.argv = ["bench.py"]
+import importlib.util
+spec = importlib.util.spec_from_file_location("rt_bench", {bench!r})
+b = importlib.util.module_from_spec(spec); spec.loader.exec_module(b)
+class C:
+    rank, world, distributed = 0, 1, False
+c = C()
+args = b.parse([])
+state = {{"assembly": {{"rccl_p2p": {{"ms_per_step": 0.25, "frame_check": "bit-exact"}}}}}}
+ph = b.Phases(c, 1.0, lambda: b.multi_line(args, c, state))
+ph.run("weak_scaling", lambda: time.sleep(60), state)  # hangs past the deadline
+print("not reached")
+"""
+
+
+def test_phase_watchdog_prints_line():
+    """A phase that hangs (an RCCL collective that never completes) makes rank
+    0 print the line built so far, that phase marked as a timeout, and exit 0
+    long before the hang ends."""
+    import json
+    import subprocess
+    import time
+
+    code = _WATCHDOG.format(repo=str(REPO), bench=str(REPO / "bench.py"))
+    t0 = time.monotonic()
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=50)
+    assert r.returncode == 0, r.stderr
+    assert time.monotonic() - t0 < 40
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1 and "not reached" not in r.stdout
+    line = json.loads(lines[0])
+    assert "timeout" in line["weak_scaling"]["error"]
+    assert line["ms_per_step"] == 0.25 and line["phase_errors"] == ["weak_scaling"]

@@ -177,6 +177,34 @@ def test_bench_rehearsal_assemblies(world, tmp_path):
     assert bal["frame_check"] == "bit-exact" and sum(bal["rows_per_rank"]) == 512, bal
     assert line["value"] == pytest.approx(1024 * 512 / (line["ms_per_step"] * 1e-3) / 1e6,
                                           rel=2e-3)
+    # the CPU path beside the GPU numbers at N > 1 too (rank 0)
+    assert line["cpu_baseline"]["value"] > 0 and line["cpu_baseline"]["cores"] >= 1
+    assert "phase_errors" not in line, line.get("phase_errors")
+
+
+def test_bench_rehearsal_forced_failure(tmp_path):
+    """bench.py at N>1 with one assembly forced to raise on rank 1 only
+    (rank 0 then waits in that assembly's collectives until the process
+    group's timeout): the failure is recorded as {"error": ...} on every rank,
+    the other assemblies still run, and rank 0 prints one line whose value
+    comes from a bit-exact assembly."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node=2", "--master-addr=127.0.0.1", "--master-port=29534",
+           str(REPO / "bench.py"), "--gpus", "2", "--rehearse", "--steps", "3",
+           "--warmup", "1", "--width", "1024", "--height", "512", "--no-extras",
+           "--no-cpu-baseline", "--pg-timeout", "15", "--fail-assembly", "rccl_p2p:1"]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=tmp_path)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [s for s in p.stdout.splitlines() if s.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    line = json.loads(lines[0])
+    assert "error" in line["assembly"]["rccl_p2p"], line["assembly"]
+    assert line["assembly"]["xgmi_peer_store"]["frame_check"] == "bit-exact"
+    assert "assembly.rccl_p2p" in line["phase_errors"]
+    assert line["value"] and line["config"]["parallelism"].endswith(
+        ("xgmi_peer_store (rehearsal: shared cuda:0, gloo)",
+         "xgmi_peer_store_balanced (rehearsal: shared cuda:0, gloo)"))
 
 
 def _tie_scene(pkg, w, h, n, seed):
