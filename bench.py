@@ -202,6 +202,8 @@ class Ctx:
                                         timeout=timeout)
             else:
                 dist.init_process_group("gloo", timeout=timeout)
+        self.pg = None  # the data-path group: the default one until a phase fails
+        self.pg_timeout = args.pg_timeout
         self.dev = torch.device("cuda", self.gpu)
         # collectives move GPU tensors with RCCL, host copies with gloo
         self.coll_dev = self.dev if self.backend == "nccl" else torch.device("cpu")
@@ -210,9 +212,18 @@ class Ctx:
         self.stream = torch.cuda.Stream(self.dev)
         torch.cuda.set_stream(self.stream)
 
+    def renew_group(self):
+        """A fresh data-path group for the phases after a failed one: a rank
+        that raised out of a phase left the others' collectives of that phase
+        unmatched, so the old group's sequence of operations no longer lines
+        up across ranks (every rank calls this, after the agreement)."""
+        if self.distributed:
+            self.pg = self.dist.new_group(backend=self.backend,
+                                          timeout=datetime.timedelta(seconds=self.pg_timeout))
+
     def barrier(self):
         if self.distributed:
-            self.dist.barrier()
+            self.dist.barrier(group=self.pg)
 
     def clock_ramp(self, step, ms: float) -> int:
         """Untimed: repeat step() (in chunks, synchronised) until `ms` of
@@ -234,7 +245,7 @@ class Ctx:
         if not self.distributed:
             return v
         t = self.torch.tensor([v], dtype=self.torch.float64, device=self.coll_dev)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.pg)
         return float(t.item())
 
     def timed(self, step, steps: int, events=None) -> float:
@@ -330,6 +341,8 @@ class Phases:
         with self.lock:
             self.current = None
             target[key] = val if ok else {"error": err or "failed on another rank"}
+        if not ok and hasattr(self.c, "renew_group"):
+            self.c.renew_group()
         return target[key]
 
 
@@ -622,7 +635,7 @@ class Assembly:
             dst = self.band.data_ptr()
         else:
             self.shared = rowbands.SharedFrame(rt, self.row_bytes * height, self.row_bytes,
-                                               c.rank, handle_device=c.coll_dev)
+                                               c.rank, handle_device=c.coll_dev, group=c.pg)
             if not self.shared.ok:
                 self.error = self.shared.error
                 return
@@ -644,13 +657,14 @@ class Assembly:
         if self.how == "rccl_p2p":
             if c.backend == "nccl":
                 for q in self.rowbands.assemble_frame(self.frame, self.band, self.height, c.world,
-                                                      c.rank, async_op=True, bands=self.bands):
+                                                      c.rank, async_op=True, bands=self.bands,
+                                                      group=c.pg):
                     q.wait()  # the stream waits; the host does not
             else:
                 c.sync()
                 hf = self.host_frame
                 self.rowbands.assemble_frame(hf, self.band.cpu(), self.height, c.world, c.rank,
-                                             bands=self.bands)
+                                             bands=self.bands, group=c.pg)
                 if self.root:  # the other ranks' rows, host -> device
                     for r in range(1, c.world):
                         rb, re = self.bands[r]
@@ -660,10 +674,10 @@ class Assembly:
             # finished: a one-element all-reduce behind the render on each
             # rank's stream (RCCL), or a host barrier after a sync (gloo)
             if c.backend == "nccl":
-                c.dist.all_reduce(self.signal, async_op=True).wait()
+                c.dist.all_reduce(self.signal, async_op=True, group=c.pg).wait()
             else:
                 c.sync()
-                c.dist.barrier()
+                c.dist.barrier(group=c.pg)
 
     def step(self):
         self.render_only()
@@ -683,13 +697,13 @@ class Assembly:
             c.sync()
             ok.fill_(int(c.torch.equal(ref, self.frame)))
             del ref
-        c.dist.broadcast(ok, 0)
+        c.dist.broadcast(ok, 0, group=c.pg)
         return "bit-exact" if int(ok.item()) else "MISMATCH"
 
     def close(self):
         if self.shared is not None:
             self.c.sync()
-            self.shared.close()
+            self.shared.close(group=self.c.pg)
 
 
 def _wrap_device(c: Ctx, ptr: int, rows, width, fmt):
@@ -749,7 +763,7 @@ def calibrate_peer_store(args, c, pkg, rt, ds, width, height, fmt):
     if height < 2 * 16 * c.world:
         return None
     shared = rowbands.SharedFrame(rt, row_bytes * height, row_bytes, c.rank,
-                                  handle_device=c.coll_dev)
+                                  handle_device=c.coll_dev, group=c.pg)
     try:
         if not shared.ok:
             return None
@@ -777,11 +791,11 @@ def calibrate_peer_store(args, c, pkg, rt, ds, width, height, fmt):
             fixed = max(0.0, t1 - slope * n1)
         mine = c.torch.tensor([fixed, slope], dtype=c.torch.float64, device=c.coll_dev)
         every = [c.torch.empty_like(mine) for _ in range(c.world)]
-        c.dist.all_gather(every, mine)
+        c.dist.all_gather(every, mine, group=c.pg)
         return [(float(e[0]), float(e[1])) for e in every]
     finally:
         c.sync()
-        shared.close()
+        shared.close(group=c.pg)
 
 
 def measure_host_frame(args, c: Ctx, pkg, rt, scene, w, h, fmt="i32x4"):
@@ -806,7 +820,7 @@ def measure_host_frame(args, c: Ctx, pkg, rt, scene, w, h, fmt="i32x4"):
         if c.rank == 0:
             shm = shared_memory.SharedMemory(create=True, size=nbytes)
             name = [shm.name]
-        c.dist.broadcast_object_list(name, 0)
+        c.dist.broadcast_object_list(name, 0, group=c.pg)
         if c.rank != 0:
             shm = shared_memory.SharedMemory(name=name[0])
             resource_tracker.unregister(shm._name, "shared_memory")  # rank 0 unlinks it
@@ -817,7 +831,7 @@ def measure_host_frame(args, c: Ctx, pkg, rt, scene, w, h, fmt="i32x4"):
         def step():
             if re > rb:
                 rt.render(scene, w, h, rows=(rb, re), fmt=fmt, out=band)
-            c.dist.barrier()
+            c.dist.barrier(group=c.pg)
         for _ in range(max(1, args.warmup)):
             step()
         ms = c.timed(step, args.steps)
@@ -830,7 +844,7 @@ def measure_host_frame(args, c: Ctx, pkg, rt, scene, w, h, fmt="i32x4"):
             c.sync()
             ok.fill_(int(np.array_equal(ref.cpu().numpy().view(frame.dtype), frame)))
             del ref, keep
-        c.dist.broadcast(ok, 0)
+        c.dist.broadcast(ok, 0, group=c.pg)
         pkg.host_unregister(frame)
         return {"scope": "rt_render per rank (scene upload + render + band download over its "
                          "own PCIe link) into one shared page-locked host frame, then a barrier",
@@ -842,7 +856,7 @@ def measure_host_frame(args, c: Ctx, pkg, rt, scene, w, h, fmt="i32x4"):
         del frame
         if shm is not None:
             shm.close()
-            c.dist.barrier()
+            c.dist.barrier(group=c.pg)
             if c.rank == 0:
                 shm.unlink()
 

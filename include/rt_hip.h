@@ -69,7 +69,11 @@ typedef struct rt_scene {
 typedef struct rt_timing {
     double total_us;    /* host wall time of the whole call (the reference's
                            timer scope, MainState.cpp:662-894) */
-    double upload_us;   /* H2D scene (+ origins) copy, HIP events */
+    double upload_us;   /* H2D scene (+ origins) copy, HIP events; with
+                           explicit origins on the automatic path it also
+                           covers their on-device grid check (a small kernel,
+                           a 4-byte read-back and a stream sync before the
+                           render, so the two are serialised) */
     double kernel_us;   /* all render kernels, HIP events */
     double download_us; /* D2H frame copy, HIP events */
     int32_t path;       /* RT_PATH_BINNED or RT_PATH_GENERIC actually used */

@@ -10,6 +10,16 @@
 //   rt_headless [--scene 1|2|3] [--seed S] [--width W] [--height H]
 //               [--synthetic N M k] [--rows A B] [--ppm out.ppm] [--repeat R]
 //               [--bands B] [--devices D] [--device-scene]
+//               [--format i32x4|rgba8]
+//
+// --format rgba8 asks the library for the Texture's pixel format directly
+// (RT_FORMAT_RGBA8: one uint32 per pixel, bytes R, G, B, 0xFF -- the
+// (uint8_t) wrap and masks of generateImageFromPixels, MainState.cpp:
+// 984-994, 1023-1037).  The buffer is what SDL_CreateRGBSurfaceFrom(buf, w,
+// h, 32, 4 * w, 0xff, 0xff00, 0xff0000, 0xff000000) wraps without a copy
+// (INTEGRATION.md), replacing the per-pixel SDL_FillRect loop; here the PPM
+// dump reads it the same way.  The printed hash is FNV-1a-64 over the uint32
+// words.
 //
 // --device-scene (with --synthetic, one band) builds the scene on the GPU
 // with rt_scene_synthetic_device, renders it with
@@ -43,15 +53,23 @@ uint64_t fnv1a(const int32_t* v, size_t n) {
     return h;
 }
 
-bool write_ppm(const std::string& path, const std::vector<int32_t>& frame, int w, int h) {
+// PPM of a frame in either format: int32x4 pixels take the Texture's
+// (uint8_t) wrap (MainState.cpp:1026-1028); RGBA8 words already hold it
+// (byte 0 red, 1 green, 2 blue: the surface masks 0xff, 0xff00, 0xff0000).
+bool write_ppm(const std::string& path, const std::vector<int32_t>& frame, int w, int h,
+               bool rgba8) {
     FILE* f = std::fopen(path.c_str(), "wb");
     if (!f) return false;
     std::fprintf(f, "P6\n%d %d\n255\n", w, h);
     std::vector<unsigned char> row(3 * (size_t)w);
     for (int y = 0; y < h; ++y) {
-        for (int x = 0; x < w; ++x)
-            for (int c = 0; c < 3; ++c)  // (uint8_t) wrap, MainState.cpp:1026-1028
-                row[3 * x + c] = static_cast<unsigned char>(frame[4 * ((size_t)y * w + x) + c]);
+        for (int x = 0; x < w; ++x) {
+            const size_t px = (size_t)y * w + x;
+            for (int c = 0; c < 3; ++c)
+                row[3 * x + c] =
+                    rgba8 ? static_cast<unsigned char>((uint32_t)frame[px] >> (8 * c))
+                          : static_cast<unsigned char>(frame[4 * px + c]);
+        }
         std::fwrite(row.data(), 1, row.size(), f);
     }
     std::fclose(f);
@@ -66,7 +84,7 @@ struct Band {
 
 // --device-scene: the scene built and rendered on the device, frame read back.
 int render_device_scene(Band& band, int width, int height, int row_begin, int row_end, int n,
-                        int m, unsigned seed, float k, const float ray_dir[4],
+                        int m, unsigned seed, float k, const float ray_dir[4], int32_t fmt,
                         std::vector<int32_t>& pixels) {
     float *so = nullptr, *sr = nullptr, *sc = nullptr, *cv = nullptr, *cc = nullptr;
     int32_t* out = nullptr;
@@ -82,7 +100,7 @@ int render_device_scene(Band& band, int width, int height, int row_begin, int ro
         rt_scene scene{so, sr, sc, n, cv, cc, m, nullptr, 0};
         if (rc == RT_OK)
             rc = rt_render_device(band.ctx, &scene, ray_dir, nullptr, width, height, row_begin,
-                                  row_end, RT_FORMAT_I32X4, RT_PATH_AUTO, out, nullptr);
+                                  row_end, fmt, RT_PATH_AUTO, out, nullptr);
         if (rc == RT_OK && hipDeviceSynchronize() == hipSuccess &&
             hipMemcpy(pixels.data(), out, pixels.size() * sizeof(int32_t),
                       hipMemcpyDeviceToHost) == hipSuccess) {
@@ -114,6 +132,7 @@ int main(int argc, char** argv) {
     int row_begin = 0, row_end = -1;
     int n_bands = 1, n_devices = 1;
     bool device_scene = false;
+    int32_t fmt = RT_FORMAT_I32X4;
     std::string ppm;
     for (int i = 1; i < argc; ++i) {
         std::string a = argv[i];
@@ -140,6 +159,15 @@ int main(int argc, char** argv) {
         else if (a == "--bands") n_bands = std::atoi(next());
         else if (a == "--devices") n_devices = std::atoi(next());
         else if (a == "--device-scene") device_scene = true;
+        else if (a == "--format") {
+            const std::string v = next();
+            if (v == "i32x4") fmt = RT_FORMAT_I32X4;
+            else if (v == "rgba8") fmt = RT_FORMAT_RGBA8;
+            else {
+                std::fprintf(stderr, "--format takes i32x4 or rgba8\n");
+                return 2;
+            }
+        }
         else {
             std::fprintf(stderr, "unknown option %s\n", a.c_str());
             return 2;
@@ -195,9 +223,12 @@ int main(int argc, char** argv) {
     float ray_dir[4];
     rt_primary_ray_dir(ray_dir);  // (0,0,-1,-1), MainState.cpp:37-39
     rt_scene scene{so.data(), sr.data(), sc.data(), ns, cv.data(), cc.data(), nc, nullptr, 0};
-    std::vector<int32_t> pixels(4 * (size_t)width * rows);
+    // MainState::pixels (MainState.h:86, reserved at :215): 4 ints per pixel,
+    // or the Texture's one RGBA8 word per pixel
+    const bool rgba8 = fmt == RT_FORMAT_RGBA8;
+    std::vector<int32_t> pixels((rgba8 ? 1 : 4) * (size_t)width * rows);
     if (device_scene) return render_device_scene(bands[0], width, height, row_begin, row_end,
-                                                 syn_n, syn_m, seed, syn_k, ray_dir, pixels);
+                                                 syn_n, syn_m, seed, syn_k, ray_dir, fmt, pixels);
     // rt_render_multi: one host thread and one context per band, each band's
     // rows written straight into `pixels` (same row split as `bands`)
     std::vector<rt_ctx*> ctxs;
@@ -207,7 +238,7 @@ int main(int argc, char** argv) {
     for (int r = 0; r < repeat && status == 0; ++r) {
         std::printf("HIP Ray Tracer Begin\n");
         rc = rt_render_multi(ctxs.data(), n_bands, &scene, ray_dir, nullptr, width, height,
-                             row_begin, row_end, RT_FORMAT_I32X4, pixels.data(), timings.data());
+                             row_begin, row_end, fmt, pixels.data(), timings.data());
         if (rc != RT_OK) {
             std::fprintf(stderr, "rt_render_multi failed: %s\n", rt_error_string(rc));
             status = 1;
@@ -228,10 +259,10 @@ int main(int argc, char** argv) {
         }
     }
     if (status == 0) {
-        std::printf("frame %dx%d rows [%d,%d) spheres %d cubes %d fnv1a64 %016llx\n", width,
-                    height, row_begin, row_end, ns, nc,
+        std::printf("frame %dx%d rows [%d,%d) spheres %d cubes %d %s fnv1a64 %016llx\n", width,
+                    height, row_begin, row_end, ns, nc, rgba8 ? "rgba8" : "i32x4",
                     (unsigned long long)fnv1a(pixels.data(), pixels.size()));
-        if (!ppm.empty() && !write_ppm(ppm, pixels, width, rows))
+        if (!ppm.empty() && !write_ppm(ppm, pixels, width, rows, rgba8))
             std::fprintf(stderr, "could not write %s\n", ppm.c_str());
     }
     for (Band& band : bands) rt_destroy(band.ctx);

@@ -33,7 +33,9 @@ def balanced_bands(height: int, costs) -> List[Tuple[int, int]]:
     (fixed cost a_r, cost per row s_r): the water-filling solution of
     min max_r t_r(n_r) subject to sum_r n_r = height, n_r >= 0.  Ranks whose
     fixed cost alone exceeds the common finish time get no rows.  Rounding
-    leftovers go to rank 0."""
+    leftovers go, one row at a time, to the active rank that would finish
+    its extra row soonest (never to a dropped rank); rows the float
+    solution over-assigns come back from the rank finishing last."""
     n = len(costs)
     if n == 0 or height <= 0:
         raise ValueError("bad band request")
@@ -48,8 +50,14 @@ def balanced_bands(height: int, costs) -> List[Tuple[int, int]]:
         if not drop:
             break
         active -= drop
-    rows = [int((t - a[r]) / s[r] + 1e-6) if r in active else 0 for r in range(n)]
-    rows[0] += height - sum(rows)
+    rows = [max(0, int((t - a[r]) / s[r] + 1e-6)) if r in active else 0 for r in range(n)]
+    while sum(rows) < height:
+        r = min(active, key=lambda q: (a[q] + s[q] * (rows[q] + 1), q))
+        rows[r] += 1
+    while sum(rows) > height:
+        r = max((q for q in active if rows[q] > 0), key=lambda q: (a[q] + s[q] * rows[q], -q))
+        rows[r] -= 1
+    assert all(k >= 0 for k in rows) and sum(rows) == height, rows
     bands, at = [], 0
     for k in rows:
         bands.append((at, at + k))

@@ -198,6 +198,18 @@ def test_balanced_bands():
     # a rank whose fixed cost alone exceeds the finish time gets no rows
     b = balanced_bands(100, [(0.0, 1e-6), (1.0, 1e-6)])
     assert [e - s for s, e in b] == [100, 0]
+    # ... even when it is rank 0: the leftover rows never go to a dropped rank
+    b = balanced_bands(100, [(1.0, 1e-6), (0.0, 1e-6), (0.0, 3e-6)])
+    assert b[0] == (0, 0) and sum(e - s for s, e in b) == 100 and b[-1][1] == 100
+    # every band well-formed and the rows summing to the height, whatever the costs
+    rng = np.random.default_rng(3)
+    for _ in range(200):
+        n = int(rng.integers(1, 9))
+        hgt = int(rng.integers(1, 5000))
+        costs = [(float(rng.uniform(0, 1e-4)), float(rng.uniform(1e-9, 1e-6))) for _ in range(n)]
+        b = balanced_bands(hgt, costs)
+        assert b[0][0] == 0 and b[-1][1] == hgt
+        assert all(s <= e for s, e in b) and all(x[1] == y[0] for x, y in zip(b, b[1:]))
     with pytest.raises(ValueError):
         balanced_bands(10, [(0.0, 0.0)])
 
@@ -212,6 +224,13 @@ class _FakeCtx:
         self.rank, self.world = rank, world
         self.distributed = world > 1
         self.coll_dev = torch.device("cpu")
+        self.pg = None
+        self.renewed = 0
+
+    def renew_group(self):
+        import datetime
+        self.pg = self.dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=5))
+        self.renewed += 1
 
 
 def _args(b, extra=()):
@@ -256,12 +275,21 @@ def _phases_worker(rank, world, port, out_path):
                 dist.barrier()  # rank 0 blocks here until the gloo timeout
                 return {"ms_per_step": 0.05, "frame_check": "bit-exact"}
 
+            def after():
+                # a collective on the data-path group after the one-rank
+                # failure: it must line up again (the group was renewed)
+                import torch
+                t = torch.ones(1)
+                dist.all_reduce(t, group=c.pg)
+                return {"frac": 0.5, "sum": float(t.item())}
+
             ph.run("rccl_p2p", ok_assembly, state["assembly"])
             ph.run("xgmi_peer_store", forced, state["assembly"])
             ph.run("xgmi_peer_store_balanced", one_rank, state["assembly"])
             ph.run("weak_scaling", lambda: 1 / 0, state)
-            ph.run("roofline", lambda: {"frac": 0.5}, state)
+            ph.run("roofline", after, state)
             ph.emit()
+            assert c.renewed == 3
         if rank == 0:
             with open(out_path, "w") as f:
                 f.write(buf.getvalue())
@@ -289,7 +317,7 @@ def test_phases_record_failures_gloo(tmp_path):
     assert asm["rccl_p2p"]["frame_check"] == "bit-exact"
     # value from the one assembly that completed bit-exactly
     assert line["ms_per_step"] == 0.5 and line["value"] == pytest.approx(4096 * 4096 / 0.5e-3 / 1e6, rel=1e-3)
-    assert "error" in line["weak_scaling"] and line["roofline"] == {"frac": 0.5}
+    assert "error" in line["weak_scaling"] and line["roofline"] == {"frac": 0.5, "sum": 2.0}
     assert line["phase_errors"] == ["assembly.xgmi_peer_store",
                                     "assembly.xgmi_peer_store_balanced", "weak_scaling"]
     assert line["n_gpus"] == 2 and line["metric"]

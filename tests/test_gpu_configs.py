@@ -342,21 +342,36 @@ def test_wide_tile_build_exact(pkg, rt, oracle, case):
 def test_randomized_parity_sweep(pkg, rt, oracle, seed):
     """Seeded random frames against the oracle: frame sizes from 96 to 1500
     px a side, 1 to 600 spheres and 0 to 80 cubes at random densities, row
-    bands, both formats, both tile builds, and the culls / small-scene paths
-    forced on or off -- every combination of the round's binned paths."""
+    bands, both formats, both tile builds, the depth culls forced on or left
+    at their gates, the one-kernel small-scene path on / off / forced, the
+    fused prep + coarse kernel on / off, and bin masks or box scans.  Each
+    knob is drawn independently from the seed's generator, so no two are
+    tied to each other across the sweep."""
     rng = np.random.default_rng(1000 + seed)
     w = int(rng.integers(96, 1500))
     h = int(rng.integers(96, 1100))
-    ns = int(rng.integers(1, 600)) if seed % 4 else int(rng.integers(1, 40))
-    nc = int(rng.integers(0, 80)) if seed % 4 else int(rng.integers(0, 6))
+    few = rng.random() < 0.25
+    ns = int(rng.integers(1, 40)) if few else int(rng.integers(1, 600))
+    nc = int(rng.integers(0, 6)) if few else int(rng.integers(0, 80))
     k = float(rng.uniform(0.3, 6.0)) * w / 640
     scene = pkg.Scene.synthetic(w, h, ns, nc, seed=seed, k=k)
-    rows = (0, h) if seed % 3 else (int(rng.integers(0, h // 2)), int(rng.integers(h // 2 + 1, h + 1)))
-    fmt = "rgba8" if seed % 5 == 0 else "i32x4"
+    band = rng.random() < 0.35
+    rows = ((int(rng.integers(0, h // 2)), int(rng.integers(h // 2 + 1, h + 1))) if band
+            else (0, h))
+    fmt = "rgba8" if rng.random() < 0.25 else "i32x4"
+    tile = int(rng.integers(1, 3))
+    small_fused = int(rng.integers(0, 3))
+    cull_all = bool(rng.integers(0, 2))
+    fused_bin = int(rng.integers(0, 2))
+    bin_masks = bool(rng.random() < 0.75)
+    knobs = dict(tile=tile, small_fused=small_fused, cull_all=cull_all, fused_bin=fused_bin,
+                 bin_masks=bin_masks)
     try:
-        rt.set_tile_variant(1 + seed % 2)
-        rt.set_small_fused((2, 0, 1)[seed % 3])
-        if seed % 2:  # every depth cull forced on, in every bin and frame
+        rt.set_tile_variant(tile)
+        rt.set_small_fused(small_fused)
+        rt.set_fused_bin(fused_bin)
+        rt.set_bin_masks(bin_masks)
+        if cull_all:  # every depth cull forced on, in every bin and frame
             rt.set_coarse_cull(1)
             rt.set_coarse_cull_tri(1)
             rt.set_coarse_cull_overdraw(0)
@@ -364,6 +379,8 @@ def test_randomized_parity_sweep(pkg, rt, oracle, seed):
     finally:
         rt.set_tile_variant(0)
         rt.set_small_fused(1)
+        rt.set_fused_bin(-1)
+        rt.set_bin_masks(True)
         rt.set_coarse_cull(-1)
         rt.set_coarse_cull_tri(-1)
         rt.set_coarse_cull_overdraw(-1)
@@ -371,4 +388,4 @@ def test_randomized_parity_sweep(pkg, rt, oracle, seed):
     want = oracle.trace(scene, w, h, rows=rows, threads=THREADS)
     if fmt == "rgba8":
         want = oracle.pack_rgba8(want)
-    assert np.array_equal(got, want), (seed, w, h, ns, nc, k, rows, fmt)
+    assert np.array_equal(got, want), (seed, w, h, ns, nc, k, rows, fmt, knobs)

@@ -404,6 +404,46 @@ def test_headless_cpp_driver(pkg, scene_id, tmp_path):
     assert np.array_equal(rgb, g["frame"][..., :3].astype(np.uint8))
 
 
+def _fnv1a64_words(words: np.ndarray) -> int:
+    h = 0xcbf29ce484222325
+    for w in words.ravel().tolist():
+        h = ((h ^ (w & 0xffffffff)) * 0x100000001b3) & 0xffffffffffffffff
+    return h
+
+
+@pytest.mark.parametrize("scene_id,bands", [(1, 1), (2, 1), (3, 1), (3, 3)])
+def test_headless_cpp_driver_rgba8(pkg, oracle, scene_id, bands, tmp_path):
+    """The C++ host asking for the Texture format (rt_headless --format rgba8:
+    rt_render_multi with RT_FORMAT_RGBA8 into a uint32 buffer, the layout
+    SDL_CreateRGBSurfaceFrom(buf, w, h, 32, 4 w, 0xff, 0xff00, 0xff0000,
+    0xff000000) wraps) gets exactly the oracle's Texture
+    packing of the golden frame (MainState.cpp:1023-1037): the printed hash
+    over the words and the PPM it writes from them."""
+    import subprocess
+
+    exe = Path(pkg.library_path()).parent / "rt_headless"
+    if not exe.exists():
+        pytest.skip("rt_headless not built")
+    g = load_golden(f"scene{scene_id}_640x480")
+    want = oracle.pack_rgba8(g["frame"])
+    ppm = tmp_path / "texture.ppm"
+    env = dict(os.environ)
+    env["LD_LIBRARY_PATH"] = str(exe.parent) + ":" + env.get("LD_LIBRARY_PATH", "")
+    r = subprocess.run([str(exe), "--scene", str(scene_id), "--seed", "1", "--format", "rgba8",
+                        "--bands", str(bands), "--ppm", str(ppm)],
+                       capture_output=True, text=True, env=env, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert f"rgba8 fnv1a64 {_fnv1a64_words(want):016x}" in r.stdout, r.stdout
+    data = ppm.read_bytes()
+    header = b"P6\n640 480\n255\n"
+    assert data.startswith(header)
+    rgb = np.frombuffer(data[len(header):], np.uint8).reshape(480, 640, 3)
+    words = want.astype(np.uint32)
+    assert np.array_equal(rgb, np.stack([(words >> (8 * c)) & 0xff for c in range(3)],
+                                        -1).astype(np.uint8))
+    assert np.all((words >> 24) == 0xff)
+
+
 @pytest.mark.parametrize("args", [["--synthetic", "256", "64", "6.4", "--width", "1024",
                                    "--height", "768"],
                                   ["--synthetic", "40", "5", "2", "--width", "999",

@@ -243,6 +243,41 @@ def test_triangle_t_bounds_hold(pkg, oracle, tile):
     assert n_checked > 10000
 
 
+@pytest.mark.parametrize("tile", [(16, 16), (64, 4)])
+def test_triangle_t_bounds_hold_far_from_origin(pkg, oracle, tile):
+    """The same bounds where their error margin is largest: the margin grows
+    with the pixel coordinates (M0 + Mx |x| + My |y|), and configs 4 and 5
+    put tiles at x, y up to 16383.  Triangles of every kind are moved to
+    4000-16200 px from the origin on a 16384 x 16384 frame."""
+    w = h = 16384
+    tw, th = tile
+    rng = np.random.default_rng(71 + tw)
+    n_checked = 0
+    for v in random_triangles(rng, 176, 160, 150):
+        off = np.float32([rng.uniform(4000, 16000), rng.uniform(4000, 16000), 0.0])
+        v = (v + off).astype(np.float32)
+        ok, box, _ = pkg.debug_triangle_prep(v[0], v[1], v[2], RAY_DIR, w, 0, h)
+        if not ok or box[0] > box[2]:
+            continue
+        for _ in range(6):
+            tx = int(rng.integers(max(box[0] - tw, 0), box[2] + 1)) // tw * tw
+            ty = int(rng.integers(max(box[1] - th, 0), box[3] + 1)) // th * th
+            b = pkg.debug_triangle_t_bounds(v[0], v[1], v[2], RAY_DIR, w, 0, h,
+                                            tx, tx + tw - 1, ty, ty + th - 1)
+            if b is None:
+                continue
+            ts = oracle.tri_t_grid(v[0], v[1], v[2], RAY_DIR, tx, ty, tw, th)
+            hit = ~np.isnan(ts)
+            if not hit.any():
+                continue
+            lo, hi = b
+            assert (ts[hit] >= lo).all() and (ts[hit] <= hi).all(), (v, tx, ty, lo, hi)
+            f = ts[hit].astype(np.float32)
+            assert (f >= np.float32(lo)).all() and (f <= np.float32(hi)).all()
+            n_checked += int(hit.sum())
+    assert n_checked > 10000
+
+
 def test_sphere_box_and_tile_classifier_are_conservative(pkg, oracle):
     w, h = 160, 128
     shapes = classified_shapes(pkg)

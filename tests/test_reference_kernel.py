@@ -36,6 +36,17 @@ def refk(rt):
     k.close()
 
 
+# Pixels where the reference's own kernel differs from its CPU path (the
+# golden frame), and the largest channel difference: the fp32-vs-fp64
+# triangle test (silhouette edges through pixel centres) and
+# the device library's dot order.  The survey's probe saw 33 / 33 / 0 on
+# scenes 1-3 with an x86 build of the same kernel (glm's dot); on gfx950 the
+# fma-chained dot adds 2 pixels to scene 3.
+KERNEL_VS_CPU = {"scene1_640x480": (33, 205), "scene2_640x480": (33, 202),
+                 "scene3_640x480": (2, 1), "config1_512x512": (0, 0),
+                 "config2_1920x1080": (3, 1), "config2s_1920x1080": (1, 1)}
+
+
 @pytest.mark.parametrize("name", SMALL_FIXTURES)
 def test_reference_kernel_golden_scenes(refk, oracle, name):
     """Reference scenes 1-3 (MainState.cpp:419-639) and configs 1-2."""
@@ -46,9 +57,10 @@ def test_reference_kernel_golden_scenes(refk, oracle, name):
     want = oracle.trace_cl_gfx950(scene, w, h, ray_dir=g["ray_dir"])
     assert not diff_report(got, want), diff_report(got, want)
     # the kernel is not the parity target: where it differs from the CPU path
-    # (the golden frame) is the fp32-vs-fp64 triangle test and the dot order
+    # (the golden frame), exactly
     cpu_diff = int((got != g["frame"]).any(-1).sum())
-    assert cpu_diff < 0.01 * w * h, cpu_diff
+    max_diff = int(np.abs(got.astype(np.int64) - g["frame"]).max())
+    assert (cpu_diff, max_diff) == KERNEL_VS_CPU[name]
 
 
 @pytest.mark.parametrize("case", sorted(EDGE_CASES))
