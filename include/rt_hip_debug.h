@@ -68,12 +68,6 @@ int rt_debug_set_small_path(rt_ctx* ctx, int enable);
  * grid is resident at once, 2 = on every frame size (tests), 0 = prep_kernel
  * + trace_small_kernel (A/B and tests).  Needs the small path (above). */
 int rt_debug_set_small_fused(rt_ctx* ctx, int enable);
-/* Big scenes (> 512 primitives) whose boxes, classifiers and depth data fit a
- * workgroup's LDS (48 B per primitive + 48 per triangle + 32 per sphere, up to
- * RT_FUSE_LDS bytes): 1 = prep and coarse binning as one kernel
- * (bin_fused_kernel: every workgroup preps the scene into LDS), 0 = prep_kernel
- * then coarse3_kernel (the default); negative = the build's default. */
-int rt_debug_set_fused_bin(rt_ctx* ctx, int enable);
 /* Coarse depth cull of sphere candidates in coarse bins with at least
  * `enable` sphere candidates (1 = every bin, 0 = off: every candidate the tile
  * classifier keeps stays; negative = the build's default; A/B and tests). */

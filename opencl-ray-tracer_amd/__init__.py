@@ -156,7 +156,6 @@ def library() -> ctypes.CDLL:
         "rt_debug_set_coarse_cull_tri": (ctypes.c_int, [vp, ctypes.c_int]),
         "rt_debug_set_coarse_cull_overdraw": (ctypes.c_int, [vp, ctypes.c_int]),
         "rt_debug_set_small_fused": (ctypes.c_int, [vp, ctypes.c_int]),
-        "rt_debug_set_fused_bin": (ctypes.c_int, [vp, ctypes.c_int]),
         "rt_debug_triangle_t_bounds": (ctypes.c_int, [vp, vp, vp, vp, i32, i32, i32, i32, i32,
                                                       i32, i32, vp]),
         "rt_debug_triangle_box_wide": (ctypes.c_int, [vp, vp, vp, vp, i32, i32, i32, vp, vp]),
@@ -505,13 +504,6 @@ class RayTracer:
         """Diagnostics: coarse-list byte budget (0 = default); frames over it
         render as internal row bands."""
         _check(library().rt_debug_set_list_budget(self._ctx, nbytes), "rt_debug_set_list_budget")
-
-    def set_fused_bin(self, enable: int) -> None:
-        """Big scenes that fit a workgroup's LDS: prep + coarse binning as one
-        kernel (1, default) or two (0); negative = the build's default
-        (diagnostics / tests)."""
-        _check(library().rt_debug_set_fused_bin(self._ctx, int(enable)),
-               "rt_debug_set_fused_bin")
 
     def set_small_path(self, enable: bool) -> None:
         """Scenes of at most 512 primitives: trace_small_kernel (default) or the

@@ -60,9 +60,6 @@
 #ifndef RT_SMALL_FUSED
 #define RT_SMALL_FUSED 1  // default of rt_debug_set_small_fused
 #endif
-#ifndef RT_FUSED_BIN
-#define RT_FUSED_BIN 0  // default of rt_debug_set_fused_bin (measured: DESIGN.md §3)
-#endif
 #ifndef RT_COARSE_CULL_OVERDRAW
 #define RT_COARSE_CULL_OVERDRAW 5  // default of rt_debug_set_coarse_cull_overdraw: ... in frames
                                    // whose primitive boxes cover the frame >= 5 times
@@ -89,9 +86,6 @@ struct rt_ctx {
     // lists would exceed this is rendered as internal row bands
     int64_t list_budget = (int64_t)4 << 30;
     bool bin_masks = RT_BIN_MASKS != 0;  // separable bin masks (false: coarse scans every box)
-    // big scenes whose boxes, classifiers and depth data fit a workgroup's
-    // LDS: prep + coarse as one kernel (bin_fused_kernel)
-    bool fused_bin = RT_FUSED_BIN != 0;
     bool small_path = true;  // <= 64 x RT_SMALL_CHUNKS primitives: trace_small_kernel
     // <= 64 x RT_FUSED_CHUNKS primitives on frames whose grid is resident at
     // once: frame_small_kernel (1; 2 = on every frame size, tests; 0 = off)
@@ -686,12 +680,6 @@ int rt_debug_triangle_t_bounds(const float v0[3], const float v1[3], const float
                        &bad, &d))
         return 0;
     return tri_t_bounds(d, xa, xb, ya, yb, &out[0], &out[1]) ? 1 : 0;
-}
-
-int rt_debug_set_fused_bin(rt_ctx* ctx, int enable) {
-    if (!ctx) return RT_ERR_INVALID_ARG;
-    ctx->fused_bin = enable < 0 ? RT_FUSED_BIN != 0 : enable != 0;
-    return RT_OK;
 }
 
 int rt_debug_set_small_fused(rt_ctx* ctx, int enable) {

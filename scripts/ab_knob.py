@@ -60,7 +60,7 @@ def main():
     ap.add_argument("--knob", default="coarse_cull",
                     choices=("coarse_cull", "coarse_cull_tri", "coarse_cull_overdraw", "tile_variant",
                              "small_fused",
-                             "small_path", "bin_masks", "fused_bin",
+                             "small_path", "bin_masks",
                              "trace_mode"))
     ap.add_argument("--values", default="0,1")
     ap.add_argument("--configs", default="c3,c5d,c5s,band8")
@@ -84,13 +84,12 @@ def main():
               "tile_variant": rt.set_tile_variant,
               "small_fused": rt.set_small_fused,
               "small_path": rt.set_small_path,
-              "bin_masks": rt.set_bin_masks, "fused_bin": rt.set_fused_bin,
-              "trace_mode": rt.set_trace_mode}[args.knob]
+              "bin_masks": rt.set_bin_masks, "trace_mode": rt.set_trace_mode}[args.knob]
     setters = {"coarse_cull": rt.set_coarse_cull, "coarse_cull_tri": rt.set_coarse_cull_tri,
                "coarse_cull_overdraw": rt.set_coarse_cull_overdraw,
                "tile_variant": rt.set_tile_variant, "small_fused": rt.set_small_fused,
                "small_path": rt.set_small_path, "bin_masks": rt.set_bin_masks,
-               "fused_bin": rt.set_fused_bin, "trace_mode": rt.set_trace_mode}
+               "trace_mode": rt.set_trace_mode}
     for kv in args.fixed:
         name, val = kv.split("=")
         setters[name](int(val))

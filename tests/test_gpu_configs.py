@@ -343,8 +343,8 @@ def test_randomized_parity_sweep(pkg, rt, oracle, seed):
     """Seeded random frames against the oracle: frame sizes from 96 to 1500
     px a side, 1 to 600 spheres and 0 to 80 cubes at random densities, row
     bands, both formats, both tile builds, the depth culls forced on or left
-    at their gates, the one-kernel small-scene path on / off / forced, the
-    fused prep + coarse kernel on / off, and bin masks or box scans.  Each
+    at their gates, the one-kernel small-scene path on / off / forced, and bin
+    masks or box scans.  Each
     knob is drawn independently from the seed's generator, so no two are
     tied to each other across the sweep."""
     rng = np.random.default_rng(1000 + seed)
@@ -362,14 +362,11 @@ def test_randomized_parity_sweep(pkg, rt, oracle, seed):
     tile = int(rng.integers(1, 3))
     small_fused = int(rng.integers(0, 3))
     cull_all = bool(rng.integers(0, 2))
-    fused_bin = int(rng.integers(0, 2))
     bin_masks = bool(rng.random() < 0.75)
-    knobs = dict(tile=tile, small_fused=small_fused, cull_all=cull_all, fused_bin=fused_bin,
-                 bin_masks=bin_masks)
+    knobs = dict(tile=tile, small_fused=small_fused, cull_all=cull_all, bin_masks=bin_masks)
     try:
         rt.set_tile_variant(tile)
         rt.set_small_fused(small_fused)
-        rt.set_fused_bin(fused_bin)
         rt.set_bin_masks(bin_masks)
         if cull_all:  # every depth cull forced on, in every bin and frame
             rt.set_coarse_cull(1)
@@ -379,7 +376,6 @@ def test_randomized_parity_sweep(pkg, rt, oracle, seed):
     finally:
         rt.set_tile_variant(0)
         rt.set_small_fused(1)
-        rt.set_fused_bin(-1)
         rt.set_bin_masks(True)
         rt.set_coarse_cull(-1)
         rt.set_coarse_cull_tri(-1)
