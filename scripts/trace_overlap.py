@@ -14,18 +14,18 @@ import sys
 
 def main(path, fmt="i32x4"):
     rows = list(csv.DictReader(open(path)))
-    tag = "ILi0ELi0E" if fmt == "i32x4" else "ILi0ELi1E"
+    tag = "trace3_kernel<0, 0>" if fmt == "i32x4" else "trace3_kernel<0, 1>"
     ks = []
     for r in rows:
         n = r["Kernel_Name"]
-        kind = ("trace" if "trace3_kernel" in n and tag in n else "prep" if "prep_kernel" in n
+        kind = ("trace" if tag in n else "prep" if "prep_kernel" in n
                 else "coarse" if "coarse3_kernel" in n else None)
         if kind:
             ks.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), kind,
                        r["Queue_Id"], n))
     ks.sort()
     traces = [k for k in ks if k[2] == "trace"]
-    # the longest run of traces dispatched within 200 us of each other
+    # runs of traces dispatched within 200 us of each other
     runs, cur = [], [traces[0]]
     for a, b in zip(traces, traces[1:]):
         if b[0] - a[1] < 200_000:
@@ -34,7 +34,9 @@ def main(path, fmt="i32x4"):
             runs.append(cur)
             cur = [b]
     runs.append(cur)
-    run = max(runs, key=len)
+    # frames in flight: the longest run that uses more than one queue
+    multi = [r for r in runs if len({k[3] for k in r}) > 1 and len(r) >= 8]
+    run = max(multi or runs, key=len)
     t0, t1 = run[0][0], run[-1][1]
     inside = [k for k in ks if t0 <= k[0] and k[1] <= t1]
     dur = {kind: statistics.mean((k[1] - k[0]) / 1e3 for k in inside if k[2] == kind)
