@@ -100,6 +100,9 @@ def parse(argv=None):
                     help="N=1: frames in flight -- step i renders frame i on slot i %% S of S "
                          "(context, stream, frame buffer) slots, so one frame's prep and "
                          "binning kernels overlap the previous frame's trace (1 = one stream)")
+    ap.add_argument("--inflight-rgba8", type=int, default=3,
+                    help="the same for the texture_rgba8 leg (its trace leaves more room "
+                         "beside it: 3 slots measured best, DESIGN.md §3.4)")
     ap.add_argument("--pg-timeout", type=float, default=180.0,
                     help="N>1: seconds before a stuck collective raises / aborts")
     ap.add_argument("--phase-deadline", type=float, default=120.0,
@@ -379,19 +382,21 @@ def inflight_step(pkg, c: Ctx, ds, w, h, fmt, path, slots: int):
     return step, frames, (rts, streams)
 
 
-def measure_inflight(args, c: Ctx, pkg, ds, w, h, fmt, ref_frame):
-    """Throughput with args.inflight frames in flight (the N=1 `value`):
-    the timed region is K whole frames, every one a full prep + bin + trace
-    pass; each slot's frame is compared with the one-stream frame."""
-    step, frames, keep = inflight_step(pkg, c, ds, w, h, fmt, args.path, args.inflight)
-    for _ in range(4 * args.inflight + args.warmup):
+def measure_inflight(args, c: Ctx, pkg, ds, w, h, fmt, ref_frame, slots=None):
+    """Throughput with `slots` (default args.inflight) frames in flight (the
+    N=1 `value`): the timed region is K whole frames, every one a full prep +
+    bin + trace pass; each slot's frame is compared with the one-stream
+    frame."""
+    slots = slots or args.inflight
+    step, frames, keep = inflight_step(pkg, c, ds, w, h, fmt, args.path, slots)
+    for _ in range(4 * slots + args.warmup):
         step()
     c.sync()
     ms = c.timed(step, args.steps)
     same = all(bool(c.torch.equal(f, ref_frame)) for f in frames)
     for rt in keep[0]:
         rt.close()
-    return {"frames_in_flight": args.inflight, "ms_per_step": round(ms, 4),
+    return {"frames_in_flight": slots, "ms_per_step": round(ms, 4),
             "value": round(mrays_per_s(w * h, ms), 1),
             "frame_check": "bit-exact" if same else "MISMATCH"}
 
@@ -540,8 +545,8 @@ def run_single(args, c: Ctx, pkg):
         for _ in range(args.warmup):
             tstep()
         t_wall = c.timed(tstep, args.steps)
-        t_inf = (measure_inflight(args, c, pkg, ds, w, h, "rgba8", tex)
-                 if args.inflight > 1 else None)
+        t_inf = (measure_inflight(args, c, pkg, ds, w, h, "rgba8", tex, args.inflight_rgba8)
+                 if args.inflight_rgba8 > 1 else None)
         rt.profile(True)
         for _ in range(args.steps):
             tstep()

@@ -11,7 +11,9 @@
 
 namespace rt_internal {
 int ctx_device(const rt_ctx* ctx);
-hipStream_t ctx_stream(const rt_ctx* ctx);
+// the context's own stream, created on first use (nullptr if that fails):
+// a context used only with caller streams never takes a hardware queue
+hipStream_t ctx_stream(rt_ctx* ctx);
 }  // namespace rt_internal
 
 #endif /* RT_INTERNAL_H */

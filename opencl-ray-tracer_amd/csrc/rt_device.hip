@@ -111,7 +111,11 @@ struct rt_ctx {
 
 namespace rt_internal {
 int ctx_device(const rt_ctx* ctx) { return ctx->device; }
-hipStream_t ctx_stream(const rt_ctx* ctx) { return ctx->stream; }
+hipStream_t ctx_stream(rt_ctx* ctx) {
+    if (!ctx->stream && hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess)
+        ctx->stream = nullptr;
+    return ctx->stream;
+}
 }  // namespace rt_internal
 
 namespace {
@@ -283,10 +287,9 @@ int rt_init(int device_ordinal, rt_ctx** out_ctx) {
     if (hipDeviceGetAttribute(&ctx->n_cu, hipDeviceAttributeMultiprocessorCount,
                               device_ordinal) != hipSuccess || ctx->n_cu <= 0)
         ctx->n_cu = 256;
-    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
-        delete ctx;
-        return RT_ERR_HIP;
-    }
+    // (the context's own stream is created on first use, rt_internal::ctx_stream:
+    // every stream takes one of the device's few hardware queues, and the
+    // device API mostly runs on the caller's streams)
     for (auto& e : ctx->ev) {
         if (hipEventCreate(&e) != hipSuccess) {
             rt_destroy(ctx);
@@ -341,7 +344,8 @@ int rt_render_path(rt_ctx* ctx, const rt_scene* scene, const float ray_dir[4],
     rc = ensure(&ctx->out_buf, &ctx->out_cap, out_bytes);
     if (rc) return rc;
     char* sb = static_cast<char*>(ctx->scene_buf);
-    hipStream_t st = ctx->stream;
+    hipStream_t st = rt_internal::ctx_stream(ctx);
+    if (!st) return RT_ERR_HIP;
     HIP_TRY(hipEventRecord(ctx->ev[0], st));
     if (ns) {
         HIP_TRY(hipMemcpyAsync(sb + o_so, scene->sphere_origins, 16 * ns, hipMemcpyHostToDevice, st));
@@ -460,7 +464,8 @@ int rt_render_device(rt_ctx* ctx, const rt_scene* device_scene, const float ray_
     if (rc) return rc;
     if (path < RT_PATH_AUTO || path > RT_PATH_GENERIC) return RT_ERR_INVALID_ARG;
     HIP_TRY(hipSetDevice(ctx->device));
-    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : rt_internal::ctx_stream(ctx);
+    if (!st) return RT_ERR_HIP;
     // launch() reads origins from the band's first row
     const float* band_origins =
         device_ray_origins ? device_ray_origins + (size_t)4 * width * row_begin : nullptr;
@@ -579,9 +584,14 @@ int rt_selftest_fp32(rt_ctx* ctx, const float* host_in, int32_t n, float* host_s
     float* d = nullptr;
     HIP_TRY(hipMalloc(&d, sizeof(float) * 3 * (size_t)n));
     HIP_TRY(hipMemcpy(d, host_in, sizeof(float) * n, hipMemcpyHostToDevice));
-    fp32_selftest_kernel<<<dim3((n + 255) / 256), dim3(256), 0, ctx->stream>>>(d, n, d + n,
-                                                                            d + 2 * (size_t)n);
-    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    hipStream_t st = rt_internal::ctx_stream(ctx);
+    if (!st) {
+        (void)hipFree(d);
+        return RT_ERR_HIP;
+    }
+    fp32_selftest_kernel<<<dim3((n + 255) / 256), dim3(256), 0, st>>>(d, n, d + n,
+                                                                  d + 2 * (size_t)n);
+    HIP_TRY(hipStreamSynchronize(st));
     HIP_TRY(hipMemcpy(host_sqrt, d + n, sizeof(float) * n, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(host_div, d + 2 * (size_t)n, sizeof(float) * n, hipMemcpyDeviceToHost));
     (void)hipFree(d);

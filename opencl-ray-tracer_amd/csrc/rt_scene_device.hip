@@ -369,6 +369,7 @@ int rt_cube_build_device(rt_ctx* ctx, const rt_cube_op* device_ops,
     if (!device_op_offsets || !device_vertices_out) return RT_ERR_INVALID_ARG;
     if (hipSetDevice(rt_internal::ctx_device(ctx)) != hipSuccess) return RT_ERR_HIP;
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : rt_internal::ctx_stream(ctx);
+    if (!st) return RT_ERR_HIP;
     const int64_t n = 36 * (int64_t)num_cubes;
     cube_build_kernel<<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st>>>(
         device_ops, device_op_offsets, num_cubes,
@@ -391,6 +392,7 @@ int rt_scene_synthetic_device(rt_ctx* ctx, int32_t width, int32_t height, int32_
     if (n == 0) return RT_OK;
     if (hipSetDevice(rt_internal::ctx_device(ctx)) != hipSuccess) return RT_ERR_HIP;
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : rt_internal::ctx_stream(ctx);
+    if (!st) return RT_ERR_HIP;
     synthetic_scene_kernel<<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st>>>(
         static_cast<float>(width), static_cast<float>(height), num_spheres, num_cubes, seed, k,
         reinterpret_cast<float4*>(sphere_origins), sphere_radius,
@@ -406,6 +408,7 @@ int rt_selftest_sincosf(rt_ctx* ctx, const float* device_in, int64_t n, float* d
     if (n == 0) return RT_OK;
     if (hipSetDevice(rt_internal::ctx_device(ctx)) != hipSuccess) return RT_ERR_HIP;
     hipStream_t st = rt_internal::ctx_stream(ctx);
+    if (!st) return RT_ERR_HIP;
     sincosf_selftest_kernel<<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st>>>(
         device_in, n, device_sin, device_cos);
     if (hipGetLastError() != hipSuccess) return RT_ERR_HIP;
