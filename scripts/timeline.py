@@ -1,7 +1,7 @@
 """Per-wave timeline of one trace_kernel launch (RT_TIMELINE=1 build):
 occupancy over time, phase durations, dispatch order.  Diagnostics only.
 
-    python scripts/timeline.py opencl-ray-tracer_amd/variants/librt_hip_tl.so
+    python scripts/timeline.py opencl-ray-tracer_amd/variants/librt_hip_tl.so [mode] [fmt 0|1]
 """
 import ctypes
 import sys
@@ -13,7 +13,7 @@ REPO = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(REPO))
 
 
-def main(path, mode=0, width=4096, height=4096, spheres=256, cubes=64, seed=3):
+def main(path, mode=0, fmt=0, width=4096, height=4096, spheres=256, cubes=64, seed=3):
     import torch
     import __graft_entry__
     pkg = __graft_entry__.load_package()
@@ -33,7 +33,8 @@ def main(path, mode=0, width=4096, height=4096, spheres=256, cubes=64, seed=3):
                                      ctypes.c_void_p, ctypes.c_void_p] + \
         [ctypes.c_int32] * 6 + [ctypes.c_void_p, ctypes.c_void_p]
     d = pkg.primary_ray_dir()
-    out = torch.empty((height, width, 4), dtype=torch.int32, device=dev)
+    out = torch.empty((height, width, 4) if fmt == 0 else (height, width), dtype=torch.int32,
+                      device=dev)
     n_waves = width * height // 256  # 256-pixel wave tiles
     tl = torch.zeros((n_waves * 8,), dtype=torch.int32, device=dev)
     assert lib.rt_debug_set_timeline(ctx, ctypes.c_void_p(tl.data_ptr())) == 0
@@ -41,7 +42,7 @@ def main(path, mode=0, width=4096, height=4096, spheres=256, cubes=64, seed=3):
     stream = torch.cuda.Stream(dev)
     for _ in range(5):
         assert lib.rt_render_device(ctx, ctypes.byref(sc), d.ctypes.data, None, width, height,
-                                    0, height, 0, 0, out.data_ptr(), stream.cuda_stream) == 0
+                                    0, height, fmt, 0, out.data_ptr(), stream.cuda_stream) == 0
     torch.cuda.synchronize()
     v = tl.cpu().numpy().view(np.uint32).reshape(n_waves, 8).astype(np.int64)
     t0 = v[:, 0] - v[:, 0].min()
@@ -67,7 +68,7 @@ def main(path, mode=0, width=4096, height=4096, spheres=256, cubes=64, seed=3):
     # occupancy: waves alive per SIMD over time
     edges = np.linspace(0, span, 21)
     print("time(us)  alive-waves/SIMD  started  finished  store-issue TB/s  mean walk of finished")
-    tile_bytes = width * height * 16 // n_waves
+    tile_bytes = width * height * (16 if fmt == 0 else 4) // n_waves
     for a, b in zip(edges[:-1], edges[1:]):
         mid = (a + b) / 2
         alive = ((t0 <= mid) & (t3 > mid)).sum() / 1024
@@ -94,8 +95,9 @@ def main(path, mode=0, width=4096, height=4096, spheres=256, cubes=64, seed=3):
     cu = (xcc << 8) | ((hwid >> 8) & 0xF) | (((hwid >> 13) & 0x7) << 4)
     ids, counts = np.unique(cu, return_counts=True)
     print(f"CUs seen: {len(ids)}  waves/CU min {counts.min()} max {counts.max()}")
-    np.save(REPO / "gpurun_out" / f"timeline_m{mode}.npy", v)
+    np.save(REPO / "gpurun_out" / f"timeline_m{mode}_f{fmt}.npy", v)
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 0)
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 0,
+         int(sys.argv[3]) if len(sys.argv) > 3 else 0)
