@@ -289,7 +289,12 @@ class Phases:
     rank 0's watchdog print the line built so far, that phase marked
     {"error": "timeout ..."}, and end the process (os._exit(0)): the driver
     still gets its line when an RCCL collective hangs (RCCL would abort the
-    process only later, at --pg-timeout)."""
+    process only later, at --pg-timeout).  The other ranks then end quietly
+    with status 0 too (their own watchdog a little later, or the agreement
+    failing once rank 0 is gone), so the launcher reports success for a run
+    whose line, errors included, was printed."""
+
+    GRACE_S = 20.0  # non-root ranks outlive rank 0's deadline by this much
 
     def __init__(self, c, deadline_s: float, finish, pg_timeout_s: float = 180.0):
         self.c = c
@@ -304,36 +309,58 @@ class Phases:
             # waits here while the others' collective of that phase times out
             self.ctrl = c.dist.new_group(
                 backend="gloo", timeout=datetime.timedelta(seconds=3 * pg_timeout_s + 60))
-        if c.rank == 0:
+        if c.distributed or c.rank == 0:
             threading.Thread(target=self._watch, daemon=True).start()
 
+    def _quit(self, why: str):
+        """End this process with status 0 once the line is out (rank 0
+        prints it first, with the current phase marked as failed)."""
+        with self.lock:
+            if self.c.rank == 0 and not self.printed and self.current is not None:
+                key, target, _ = self.current
+                target[key] = {"error": why}
+            self.emit()
+        sys.stdout.flush()
+        sys.stderr.write(f"bench.py rank {self.c.rank}: {why}; exiting\n")
+        sys.stderr.flush()
+        os._exit(0)
+
     def _watch(self):
+        limit = self.deadline + (0.0 if self.c.rank == 0 else self.GRACE_S)
         while True:
             time.sleep(0.5)
             with self.lock:
                 cur = self.current
-                if cur is None or self.printed:
+                if cur is None or self.printed or time.monotonic() - cur[2] < limit:
                     continue
-                key, target, t0 = cur
-                if time.monotonic() - t0 < self.deadline:
-                    continue
-                target[key] = {"error": f"timeout: phase still running after "
-                                        f"{self.deadline:.0f} s (rank 0's watchdog)"}
-                self.emit()
-            sys.stdout.flush()
-            os._exit(0)
+            self._quit(f"timeout: phase still running after {self.deadline:.0f} s "
+                       f"(rank 0's watchdog)")
 
     def emit(self):
-        """Print the line once (rank 0)."""
-        if self.c.rank == 0 and not self.printed:
-            self.printed = True
-            print(json.dumps(self.finish()), flush=True)
+        """Print the line once (rank 0).  From the watchdog thread the main
+        thread may still be filling the state, so a failed serialisation is
+        retried before a minimal line goes out."""
+        if self.c.rank != 0 or self.printed:
+            return
+        self.printed = True
+        for attempt in range(5):
+            try:
+                text = json.dumps(self.finish())
+                break
+            except Exception as e:  # e.g. a dict resized during json.dumps
+                time.sleep(0.05)
+                text = json.dumps({"metric": METRIC, "value": None, "unit": "Mrays/s",
+                                   "n_gpus": self.c.world, "error": f"line: {e!r}"})
+        print(text, flush=True)
 
     def agree(self, ok: bool) -> bool:
         if self.ctrl is None:
             return ok
         t = self.c.torch.tensor([1 if ok else 0], dtype=self.c.torch.int32)
-        self.c.dist.all_reduce(t, op=self.c.dist.ReduceOp.MIN, group=self.ctrl)
+        try:
+            self.c.dist.all_reduce(t, op=self.c.dist.ReduceOp.MIN, group=self.ctrl)
+        except Exception as e:  # a rank is gone (rank 0 after printing, or a crash)
+            self._quit(f"a rank left the run: {type(e).__name__}")
         return bool(int(t.item()))
 
     def run(self, key: str, fn, target: dict):

@@ -359,3 +359,60 @@ def test_phase_watchdog_prints_line():
     line = json.loads(lines[0])
     assert "timeout" in line["weak_scaling"]["error"]
     assert line["ms_per_step"] == 0.25 and line["phase_errors"] == ["weak_scaling"]
+
+
+_TWO_RANKS = r"""
+import datetime, os, sys
+sys.path.insert(0, {repo!r})
+sys.argv = ["bench.py"]
+import importlib.util
+spec = importlib.util.spec_from_file_location("rt_bench", {bench!r})
+b = importlib.util.module_from_spec(spec); spec.loader.exec_module(b)
+import torch, torch.distributed as dist
+rank = int(os.environ["RANK"])
+dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=120))
+class C:
+    world, distributed, pg = 2, True, None
+c = C()
+c.rank, c.torch, c.dist = rank, torch, dist
+args = b.parse(["--gpus", "2"])
+state = {{"assembly": {{"rccl_p2p": {{"ms_per_step": 0.25, "frame_check": "bit-exact"}}}}}}
+ph = b.Phases(c, 3.0, lambda: b.multi_line(args, c, state), pg_timeout_s=120.0)
+def phase():
+    if rank == 1:
+        raise RuntimeError("rank 1 only")
+    dist.barrier()  # never joined by rank 1: would block for the 120 s timeout
+ph.run("xgmi_peer_store", phase, state["assembly"])
+print("not reached")
+"""
+
+
+def test_phase_timeout_every_rank_exits_zero(tmp_path):
+    """An exception on rank 1 while rank 0 blocks in that phase's data-path
+    collective (an RCCL collective cannot time out and recover): rank 0's
+    watchdog prints the line with the phase marked as failed and exits 0,
+    and rank 1, waiting in the agreement, ends with status 0 as well, so the
+    launcher sees a successful run whose line carries the error."""
+    import json
+    import subprocess
+    import time
+
+    code = _TWO_RANKS.format(repo=str(REPO), bench=str(REPO / "bench.py"))
+    port = _free_port()
+    procs = []
+    t0 = time.monotonic()
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK=str(r),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-c", code], stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True, env=env, cwd=tmp_path))
+    outs = [p.communicate(timeout=100) for p in procs]
+    assert time.monotonic() - t0 < 90
+    for p, (out, err) in zip(procs, outs):
+        assert p.returncode == 0, err[-2000:]
+        assert "not reached" not in out
+    lines = [l for l in outs[0][0].splitlines() if l.startswith("{")]
+    assert len(lines) == 1 and not [l for l in outs[1][0].splitlines() if l.startswith("{")]
+    line = json.loads(lines[0])
+    assert "error" in line["assembly"]["xgmi_peer_store"]
+    assert line["ms_per_step"] == 0.25 and line["phase_errors"] == ["assembly.xgmi_peer_store"]
