@@ -86,10 +86,10 @@ int rt_debug_triangle_t_bounds(const float v0[3], const float v1[3], const float
                                const float dir[4], int32_t width, int32_t row_begin,
                                int32_t row_end, int32_t xa, int32_t xb, int32_t ya, int32_t yb,
                                double out[2]);
-/* Wave-tile build used by the binned path: 0 = by frame size (64x4 tiles
- * for frames of >= 512 MiB, else 16x16), 1 = 16x16, 2 = 64x4. */
+/* Wave-tile build used by the binned path: 0 = by frame size (128x2 tiles
+ * for frames of >= 512 MiB, else 16x16), 1 = 16x16, 2 = 128x2. */
 int rt_debug_set_tile_variant(rt_ctx* ctx, int variant);
-/* The 64x4 build's triangle prep and tile shape (host culling tests). */
+/* The wide (128x2) build's triangle prep and tile shape (host culling tests). */
 int rt_debug_triangle_box_wide(const float v0[3], const float v1[3], const float v2[3],
                                const float dir[4], int32_t width, int32_t row_begin,
                                int32_t row_end, int32_t box_out[4], float cls_out[8]);

@@ -532,7 +532,7 @@ class RayTracer:
 
     def set_tile_variant(self, variant: int) -> None:
         """Diagnostics: the binned path's wave-tile build (0 = by frame size,
-        1 = 16x16, 2 = 64x4)."""
+        1 = 16x16, 2 = the wide 128x2 tiles)."""
         _check(library().rt_debug_set_tile_variant(self._ctx, int(variant)),
                "rt_debug_set_tile_variant")
 
@@ -602,7 +602,7 @@ def debug_triangle_prep(v0, v1, v2, ray_dir, width, row_begin, row_end):
 
 
 def debug_triangle_prep_wide(v0, v1, v2, ray_dir, width, row_begin, row_end):
-    """debug_triangle_prep of the 64x4-tile build (its classifier margin
+    """debug_triangle_prep of the wide-tile (128x2) build (its classifier margin
     covers 64-pixel tile spans)."""
     a = [np.ascontiguousarray(v, np.float32)[:3].copy() for v in (v0, v1, v2)]
     d = np.ascontiguousarray(ray_dir, np.float32)

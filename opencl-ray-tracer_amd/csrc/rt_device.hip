@@ -23,8 +23,9 @@
 // and directions (the reference's kernel arguments 8-9 in full generality).
 //
 // The kernels and their host launch() are in rt_trace.inc, compiled here
-// twice: 16x16 wave tiles (namespace tile16) and 64x4 tiles (tile64, frames
-// of >= 1 GiB, whose stores drain faster from 1-KiB rows).
+// twice: 16x16 wave tiles (namespace tile16) and 128x2 tiles (namespace
+// wide, frames of >= 512 MiB, whose stores drain faster from 2-KiB row
+// segments).
 // This file holds the context, the dispatcher and the C ABI.
 //
 // Build: -ffp-contract=off (and the pragma below): every operation rounds
@@ -81,7 +82,7 @@ struct rt_ctx {
     unsigned gen = 0;
     unsigned od_launches = 0;  // binned launches: picks the box-overdraw slot
     int trace_mode = 0;  // diagnostics ablation, see trace3_kernel
-    int tile_variant = 0;  // 0 = by frame size, 1 = 16x16 tiles, 2 = 64x4 tiles
+    int tile_variant = 0;  // 0 = by frame size, 1 = 16x16 tiles, 2 = the wide (128x2) tiles
     // coarse lists take 4 B x kListStride x (primitives + 16) per 64x64 bin; a frame whose
     // lists would exceed this is rendered as internal row bands
     int64_t list_budget = (int64_t)4 << 30;
@@ -189,12 +190,13 @@ int skip_k(rt_ctx* ctx, const hipEvent_t* ev) {
 
 // The kernels and launch(), once per wave-tile shape (rt_trace.inc).
 // 16x16 tiles suit frames below 512 MiB; larger frames store faster from
-// 64x4 tiles ("Wave tile shape per frame size").
+// 128x2 tiles (a lane's 4 pixels: 2 along x, 64 apart, in 2 rows; DESIGN.md
+// §3.5: 64x4 and 256x1 measured slower on configs 4 and 5).
 #ifndef RT_TILE_NARROW
 #define RT_TILE_NARROW 16
 #endif
 #ifndef RT_TILE_WIDE
-#define RT_TILE_WIDE 64
+#define RT_TILE_WIDE 128
 #endif
 #define RT_TILE_W RT_TILE_NARROW
 namespace tile16 {
@@ -202,9 +204,9 @@ namespace tile16 {
 }  // namespace tile16
 #undef RT_TILE_W
 #define RT_TILE_W RT_TILE_WIDE
-namespace tile64 {
+namespace wide {
 #include "rt_trace.inc"
-}  // namespace tile64
+}  // namespace wide
 #undef RT_TILE_W
 
 namespace {
@@ -237,20 +239,20 @@ __global__ void __launch_bounds__(256) grid_check_kernel(const float4* __restric
 }
 
 // Frames of at least this many bytes take the wide tiles (auto selection):
-// 512 MiB frames store faster from 64x4 tiles in both formats (config 5's
-// 8-rank band, config 4's half frame, a 512 MiB Texture), 384 MiB and
-// smaller ones from 16x16.
+// 512 MiB frames store faster from wide tiles in both formats (config 5's
+// 8-rank band, config 4's half frame, a 512 MiB Texture; measured with 64x4
+// tiles), 384 MiB and smaller ones from 16x16.
 constexpr int64_t kWideTileBytes = (int64_t)1 << 29;
 
-// rt_debug_set_tile_variant: 0 = by frame size, 1 = 16x16, 2 = 64x4
+// rt_debug_set_tile_variant: 0 = by frame size, 1 = 16x16, 2 = wide (128x2)
 int render_launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origins,
                   int32_t width, int32_t row_begin, int32_t row_end, int32_t fmt, int32_t path,
                   void* out, hipStream_t stream, int32_t* used_path) {
     const int64_t bytes =
         (int64_t)width * (row_end - row_begin) * (fmt == RT_FORMAT_I32X4 ? 16 : 4);
-    const bool wide =
+    const bool use_wide =
         ctx->tile_variant == 2 || (ctx->tile_variant == 0 && bytes >= kWideTileBytes);
-    return wide ? tile64::launch(ctx, s, d, origins, width, row_begin, row_end, fmt, path, out,
+    return use_wide ? wide::launch(ctx, s, d, origins, width, row_begin, row_end, fmt, path, out,
                                  stream, used_path)
                 : tile16::launch(ctx, s, d, origins, width, row_begin, row_end, fmt, path, out,
                                  stream, used_path);
@@ -634,15 +636,15 @@ int rt_debug_set_tile_variant(rt_ctx* ctx, int variant) {
     return RT_OK;
 }
 
-// The wide-tile (64x4) build's prep for the host-side culling tests.
+// The wide-tile (128x2) build's prep for the host-side culling tests.
 int rt_debug_triangle_box_wide(const float v0[3], const float v1[3], const float v2[3],
                                const float dir[4], int32_t width, int32_t row_begin,
                                int32_t row_end, int32_t box_out[4], float cls_out[8]) {
-    tile64::TriRec r{};
-    tile64::Box b{};
-    tile64::Cls k{};
+    wide::TriRec r{};
+    wide::Box b{};
+    wide::Cls k{};
     bool bad = false;
-    const bool ok = tile64::prep_triangle(v0, v1, v2, dir[0], dir[1], dir[2], width, row_begin,
+    const bool ok = wide::prep_triangle(v0, v1, v2, dir[0], dir[1], dir[2], width, row_begin,
                                           row_end, &r, &b, &k, &bad);
     box_out[0] = b.x0; box_out[1] = b.y0; box_out[2] = b.x1; box_out[3] = b.y1;
     if (cls_out) std::memcpy(cls_out, &k, sizeof k);
@@ -651,8 +653,8 @@ int rt_debug_triangle_box_wide(const float v0[3], const float v1[3], const float
 
 int rt_debug_tile_shape_wide(int32_t* w, int32_t* h) {
     if (!w || !h) return RT_ERR_INVALID_ARG;
-    *w = tile64::kWaveTile;
-    *h = tile64::kWaveTileH;
+    *w = wide::kWaveTile;
+    *h = wide::kWaveTileH;
     return RT_OK;
 }
 

@@ -30,6 +30,9 @@ def main():
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--size", type=int, default=4096)
     ap.add_argument("--format", default="i32x4", choices=("i32x4", "rgba8"))
+    ap.add_argument("--spheres", type=int, default=256)
+    ap.add_argument("--cubes", type=int, default=64)
+    ap.add_argument("--seed", type=int, default=3)
     args = ap.parse_args()
     import torch
     import __graft_entry__
@@ -40,7 +43,7 @@ def main():
     n_cu = torch.cuda.get_device_properties(0).multi_processor_count
     words = (n_cu + 31) // 32
     w = h = args.size
-    scene = pkg.Scene.synthetic(w, h, 256, 64, seed=3, k=w / 640)
+    scene = pkg.Scene.synthetic(w, h, args.spheres, args.cubes, seed=args.seed, k=w / 640)
     dev = torch.device("cuda:0")
     t = {n: torch.from_numpy(np.ascontiguousarray(getattr(scene, n))).to(dev)
          for n in ("sphere_origins", "sphere_radius", "sphere_colours", "cube_vertices",

@@ -300,7 +300,7 @@ def test_render_into_registered_host_frame(pkg, rt):
 
 @pytest.mark.parametrize("case", ["golden", "dense", "rgba8", "bands", "culled", "edges"])
 def test_wide_tile_build_exact(pkg, rt, oracle, case):
-    """The 64x4-tile build (auto-selected for frames of >= 512 MiB) forced on
+    """The wide-tile (128x2) build (auto-selected for frames of >= 512 MiB) forced on
     small frames: bit-exact against the oracle / golden frames and against
     the 16x16 build, on awkward sizes, bands, both formats and the coarse
     depth cull."""

@@ -159,7 +159,7 @@ def wide_tile_shape(pkg):
 @pytest.mark.parametrize("build", ["narrow", "wide"])
 @pytest.mark.parametrize("band", [(0, 160), (37, 121)])
 def test_triangle_box_and_tile_classifier_are_conservative(pkg, oracle, band, build):
-    """Both wave-tile builds (16x16 and 64x4 tiles; each has its own
+    """Both wave-tile builds (16x16 and 128x2 tiles; each has its own
     classifier margin for its tile span)."""
     w, h = 176, 160
     rb, re = band
@@ -169,7 +169,7 @@ def test_triangle_box_and_tile_classifier_are_conservative(pkg, oracle, band, bu
         prep = pkg.debug_triangle_prep
     else:
         tw, th = wide_tile_shape(pkg)
-        assert (tw, th) == (64, 4)
+        assert (tw, th) == (128, 2)
         shapes = [(tw, th)]
         prep = pkg.debug_triangle_prep_wide
     rng = np.random.default_rng(7 + rb)
@@ -209,7 +209,7 @@ def test_triangle_box_and_tile_classifier_are_conservative(pkg, oracle, band, bu
     assert n_inside_tiles > 0 and n_skip_tiles > 0  # the classifier does something
 
 
-@pytest.mark.parametrize("tile", [(16, 16), (64, 4)])
+@pytest.mark.parametrize("tile", [(16, 16), (64, 4), (128, 2)])
 def test_triangle_t_bounds_hold(pkg, oracle, tile):
     """The coarse depth cull's triangle bounds (tri_t_bounds): for every
     hitting pixel of a tile, the reference's fp64 t lies in [lo, hi], so its
@@ -243,7 +243,7 @@ def test_triangle_t_bounds_hold(pkg, oracle, tile):
     assert n_checked > 10000
 
 
-@pytest.mark.parametrize("tile", [(16, 16), (64, 4)])
+@pytest.mark.parametrize("tile", [(16, 16), (64, 4), (128, 2)])
 def test_triangle_t_bounds_hold_far_from_origin(pkg, oracle, tile):
     """The same bounds where their error margin is largest: the margin grows
     with the pixel coordinates (M0 + Mx |x| + My |y|), and configs 4 and 5
