@@ -100,6 +100,8 @@ def parse(argv=None):
                     help="N=1: frames in flight -- step i renders frame i on slot i %% S of S "
                          "(context, stream, frame buffer) slots, so one frame's prep and "
                          "binning kernels overlap the previous frame's trace (1 = one stream)")
+    ap.add_argument("--slot-streams", default="hip", choices=("hip", "cumask", "torch"),
+                    help=argparse.SUPPRESS)  # A/B: the frames-in-flight slots' streams
     ap.add_argument("--inflight-rgba8", type=int, default=3,
                     help="the same for the texture_rgba8 leg (its trace leaves more room "
                          "beside it: 3 slots measured best, DESIGN.md §3.4)")
@@ -218,6 +220,7 @@ class Ctx:
         # the C ABI reads as "the context's own stream".
         self.stream = torch.cuda.Stream(self.dev)
         torch.cuda.set_stream(self.stream)
+        self.slot_streams = getattr(args, "slot_streams", "hip")
 
     def renew_group(self):
         """A fresh data-path group for the phases after a failed one: a rank
@@ -389,6 +392,38 @@ def failing(args, c, name: str) -> bool:
     return what == name and (rank == "" or int(rank) == c.rank)
 
 
+class HipStreams:
+    """`n` new non-blocking HIP streams (libamdhip64 through ctypes), each
+    created now, so each takes the next hardware queue; close() destroys
+    them (after a device synchronisation by the caller)."""
+
+    def __init__(self, n: int, cu_mask_words: int = 0):
+        import ctypes
+        self.hip = ctypes.CDLL("libamdhip64.so")
+        self.hip.hipStreamCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p),
+                                                      ctypes.c_uint]
+        self.hip.hipExtStreamCreateWithCUMask.argtypes = [
+            ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]
+        self.hip.hipStreamDestroy.argtypes = [ctypes.c_void_p]
+        self.handles = []
+        for _ in range(n):
+            st = ctypes.c_void_p()
+            if cu_mask_words:  # every CU, but a stream of its own hardware queue
+                mask = (ctypes.c_uint32 * cu_mask_words)(*([0xFFFFFFFF] * cu_mask_words))
+                rc = self.hip.hipExtStreamCreateWithCUMask(ctypes.byref(st), cu_mask_words, mask)
+            else:
+                rc = self.hip.hipStreamCreateWithFlags(ctypes.byref(st), 1)  # NonBlocking
+            if rc != 0:
+                self.close()
+                raise RuntimeError(f"HIP stream creation failed ({rc})")
+            self.handles.append(st.value)
+
+    def close(self):
+        for h in self.handles:
+            self.hip.hipStreamDestroy(h)
+        self.handles = []
+
+
 def inflight_step(pkg, c: Ctx, ds, w, h, fmt, path, slots: int):
     """A step callable rendering frame i on slot i % slots: each slot has its
     own context (workspace), stream and frame buffer, so consecutive frames'
@@ -396,11 +431,20 @@ def inflight_step(pkg, c: Ctx, ds, w, h, fmt, path, slots: int):
     binning kernels of one frame run beside the previous frame's trace).
     Returns (step, frames, keep-alive)."""
     rts = [pkg.RayTracer(c.gpu) for _ in range(slots)]
-    streams = [c.torch.cuda.Stream(c.dev) for _ in range(slots)]
+    # fresh HIP streams (--slot-streams hip): torch's pool streams are handed
+    # out round-robin and may share hardware queues with streams the process
+    # made earlier, which serialises the slots
+    kind = getattr(c, "slot_streams", "hip")
+    n_words = (c.torch.cuda.get_device_properties(c.dev).multi_processor_count + 31) // 32
+    streams = (HipStreams(slots, n_words if kind == "cumask" else 0)
+               if kind in ("hip", "cumask")
+               else [c.torch.cuda.Stream(c.dev) for _ in range(slots)])
+    handles = streams.handles if isinstance(streams, HipStreams) else [st.cuda_stream
+                                                                      for st in streams]
     frames = [frame_tensor(c, h, w, fmt) for _ in range(slots)]
     fns = [rt.bind_render_device(ds, w, h, (0, h), f.data_ptr(), fmt=fmt, path=path,
-                                 stream=st.cuda_stream)
-           for rt, st, f in zip(rts, streams, frames)]
+                                 stream=st)
+           for rt, st, f in zip(rts, handles, frames)]
     n = [0]
 
     def step():
@@ -421,8 +465,11 @@ def measure_inflight(args, c: Ctx, pkg, ds, w, h, fmt, ref_frame, slots=None):
     c.sync()
     ms = c.timed(step, args.steps)
     same = all(bool(c.torch.equal(f, ref_frame)) for f in frames)
+    c.sync()
     for rt in keep[0]:
         rt.close()
+    if isinstance(keep[1], HipStreams):
+        keep[1].close()
     return {"frames_in_flight": slots, "ms_per_step": round(ms, 4),
             "value": round(mrays_per_s(w * h, ms), 1),
             "frame_check": "bit-exact" if same else "MISMATCH"}

@@ -74,11 +74,14 @@ int rt_debug_set_small_fused(rt_ctx* ctx, int enable);
 int rt_debug_set_coarse_cull(rt_ctx* ctx, int enable);
 /* Triangles join the coarse depth cull in bins whose wave tiles keep at
  * least this many candidates on average (0 = never, negative = the build's
- * default). */
+ * defaults: 4 for int32x4 renders, 2 for RGBA8 renders; a value >= 0 applies
+ * to both formats). */
 int rt_debug_set_coarse_cull_tri(rt_ctx* ctx, int min_candidates);
 /* ... and only in frames whose primitive boxes, summed, cover the frame at
  * least `frames` times (the trace is then bound by its tests rather than its
- * stores; 0 = every frame, negative = the build's default). */
+ * stores; 0 = every frame, negative = the build's defaults: 5 for int32x4
+ * renders, 0 for RGBA8 renders, whose trace is always bound by its tests).
+ * A value >= 0 applies to both formats. */
 int rt_debug_set_coarse_cull_overdraw(rt_ctx* ctx, int frames);
 /* The bounds tri_t_bounds gives the trace's computed fp64 t over pixels
  * [xa, xb] x [ya, yb] (host evaluation; returns 0 without a bound). */

@@ -65,6 +65,14 @@
 #define RT_COARSE_CULL_OVERDRAW 5  // default of rt_debug_set_coarse_cull_overdraw: ... in frames
                                    // whose primitive boxes cover the frame >= 5 times
 #endif
+#ifndef RT_COARSE_CULL_TRI_RGBA8
+#define RT_COARSE_CULL_TRI_RGBA8 2  // the triangle threshold for Texture (RGBA8) renders
+#endif
+#ifndef RT_COARSE_CULL_OVERDRAW_RGBA8
+#define RT_COARSE_CULL_OVERDRAW_RGBA8 0  // the same gate for Texture (RGBA8) renders: every
+                                         // frame (its trace is bound by its tests, not by
+                                         // its stores)
+#endif
 
 // ===========================================================================
 // Host side
@@ -98,8 +106,11 @@ struct rt_ctx {
     // triangles join the depth cull in bins whose tiles keep at least this
     // many candidates on average (0 = never)
     int coarse_cull_tri = RT_COARSE_CULL_TRI;
+    int coarse_cull_tri_rgba8 = RT_COARSE_CULL_TRI_RGBA8;  // (RGBA8 renders)
     // ... in frames whose boxes' summed area is at least this many frames
+    // (int32x4 renders; RGBA8 renders take the second gate)
     unsigned coarse_cull_overdraw = RT_COARSE_CULL_OVERDRAW;
+    unsigned coarse_cull_overdraw_rgba8 = RT_COARSE_CULL_OVERDRAW_RGBA8;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     // profiling: per render, start/stop events of the prep, coarse and trace
     // kernels, attached to the kernels' own dispatch packets
@@ -667,12 +678,15 @@ int rt_debug_set_coarse_cull(rt_ctx* ctx, int enable) {
 int rt_debug_set_coarse_cull_tri(rt_ctx* ctx, int min_candidates) {
     if (!ctx) return RT_ERR_INVALID_ARG;
     ctx->coarse_cull_tri = min_candidates < 0 ? RT_COARSE_CULL_TRI : min_candidates;
+    ctx->coarse_cull_tri_rgba8 = min_candidates < 0 ? RT_COARSE_CULL_TRI_RGBA8 : min_candidates;
     return RT_OK;
 }
 
 int rt_debug_set_coarse_cull_overdraw(rt_ctx* ctx, int frames) {
     if (!ctx) return RT_ERR_INVALID_ARG;
     ctx->coarse_cull_overdraw = frames < 0 ? RT_COARSE_CULL_OVERDRAW : (unsigned)frames;
+    ctx->coarse_cull_overdraw_rgba8 =
+        frames < 0 ? RT_COARSE_CULL_OVERDRAW_RGBA8 : (unsigned)frames;
     return RT_OK;
 }
 
