@@ -52,7 +52,7 @@ METRIC = "Mrays/sec (primary) at 4096×4096, 1/2/4/8 MI355X; % HBM-write rooflin
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec); 6.29 TB/s measured copy
 BYTES_PER_RAY = {"i32x4": 16, "rgba8": 4}
 # BASELINE.json configs by (width, height, spheres, cubes)
-CONFIG_NAMES = {(1920, 1080, 16, 4): "config2", (4096, 4096, 256, 64): "config3",
+CONFIG_NAMES = {(512, 512, 4, 1): "config1", (1920, 1080, 16, 4): "config2", (4096, 4096, 256, 64): "config3",
                 (8192, 8192, 192, 64): "config4", (16384, 16384, 4096, 0): "config5"}
 CONFIG4 = dict(width=8192, height=8192, spheres=192, cubes=64, seed=4)
 

@@ -13,6 +13,7 @@ run() {
 }
 run --width 512 --height 512 --spheres 4 --cubes 1 --seed 1           # config 1
 run --width 1920 --height 1080 --spheres 16 --cubes 4 --seed 2        # config 2
+run --width 1920 --height 1080 --spheres 16 --cubes 4 --seed 2 --format rgba8  # config 2, Texture format
 run --width 4096 --height 4096 --spheres 256 --cubes 64 --k 1          # config 3, sparse
 run --width 8192 --height 8192 --spheres 192 --cubes 64 --seed 4       # config 4, whole frame
 run --width 16384 --height 16384 --spheres 4096 --cubes 0 --seed 5     # config 5, whole frame, dense
