@@ -20,6 +20,10 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--size", type=int, default=4096)
+    ap.add_argument("--format", default="i32x4", choices=("i32x4", "rgba8"))
+    ap.add_argument("--knob", default=None,
+                    help="RayTracer setter (without set_) applied to every slot, e.g. coarse_lds")
+    ap.add_argument("--values", default="0", help="the knob's settings, interleaved")
     args = ap.parse_args()
     import torch
     import __graft_entry__
@@ -36,27 +40,36 @@ def main():
     smax = max(slots)
     ctxs = [pkg.RayTracer(0) for _ in range(smax)]
     streams = [torch.cuda.Stream(dev) for _ in range(smax)]
-    outs = [torch.empty((h, w, 4), dtype=torch.int32, device=dev) for _ in range(smax)]
-    fns = [ctxs[i].bind_render_device(ds, w, h, (0, h), outs[i].data_ptr(),
+    shape = (h, w, 4) if args.format == "i32x4" else (h, w)
+    outs = [torch.empty(shape, dtype=torch.int32, device=dev) for _ in range(smax)]
+    fns = [ctxs[i].bind_render_device(ds, w, h, (0, h), outs[i].data_ptr(), fmt=args.format,
                                       stream=streams[i].cuda_stream) for i in range(smax)]
-    res = {s: [] for s in slots}
+    values = [int(v) for v in args.values.split(",")]
+    res = {(v, s): [] for v in values for s in slots}
+    ref = None
     for r in range(args.rounds):
+        for v in values:
+            if args.knob:
+                for c in ctxs:
+                    getattr(c, "set_" + args.knob)(v)
+            for s in slots:
+                for i in range(2 * s):
+                    fns[i % s]()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for i in range(args.steps):
+                    fns[i % s]()
+                torch.cuda.synchronize()
+                res[(v, s)].append((time.perf_counter() - t0) / args.steps * 1e6)
+                if ref is None:
+                    ref = outs[0].cpu()
+                for i in range(s):
+                    assert torch.equal(outs[i].cpu(), ref), f"slot {i} differs ({args.knob}={v})"
+    for v in values:
         for s in slots:
-            for i in range(2 * s):
-                fns[i % s]()
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            for i in range(args.steps):
-                fns[i % s]()
-            torch.cuda.synchronize()
-            res[s].append((time.perf_counter() - t0) / args.steps * 1e6)
-    ref = outs[0].cpu()
-    for i in range(1, smax):
-        assert torch.equal(outs[i].cpu(), ref), f"slot {i} differs"
-    for s in slots:
-        med = statistics.median(res[s])
-        print(f"slots {s}: {med:.1f} us/frame  {w * h / med / 1e3:.1f} Grays/s  "
-              f"(min {min(res[s]):.1f})")
+            med = statistics.median(res[(v, s)])
+            print(f"{args.format} {args.knob}={v} slots {s}: {med:.1f} us/frame  "
+                  f"{w * h / med / 1e3:.1f} Grays/s  (min {min(res[(v, s)]):.1f})")
 
 
 if __name__ == "__main__":
