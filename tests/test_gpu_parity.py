@@ -246,7 +246,11 @@ def test_nonfinite_scene_falls_back_exactly(pkg, rt, oracle):
                                          (640, 480, 8, 10, 1.0), (1920, 1080, 32, 8, 3.0),
                                          (1500, 900, 65, 0, 2.0), (1920, 1080, 64, 16, 3.0),
                                          (2000, 1300, 100, 13, 2.0), (1920, 1080, 128, 32, 3.0),
-                                         (1111, 999, 300, 10, 2.0), (3000, 700, 512, 0, 3.0)])
+                                         (1111, 999, 300, 10, 2.0), (3000, 700, 512, 0, 3.0),
+                                         # frame_small_kernel's prep waves: triangles only
+                                         # (two triangle waves, no sphere wave busy); two
+                                         # sphere waves beside one triangle wave
+                                         (800, 600, 0, 10, 2.0), (900, 700, 68, 5, 2.0)])
 def test_small_scene_path(pkg, rt, oracle, w, h, ns, nc, k):
     """<= 512 primitives (up to 8 prep chunks): trace_small_kernel classifies
     each tile's candidates itself; <= 128 primitives: frame_small_kernel does
