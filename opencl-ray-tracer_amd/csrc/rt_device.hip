@@ -209,12 +209,22 @@ int skip_k(rt_ctx* ctx, const hipEvent_t* ev) {
 #ifndef RT_TILE_WIDE
 #define RT_TILE_WIDE 128
 #endif
+// nontemporal frame stores per build: bit 0 int32x4, bit 1 RGBA8
+#ifndef RT_NT_NARROW
+#define RT_NT_NARROW 2  // the 16x16 build: RGBA8 only (int32x4 measured much slower)
+#endif
+#ifndef RT_NT_WIDE
+#define RT_NT_WIDE 3
+#endif
 #define RT_TILE_W RT_TILE_NARROW
+#define RT_NT_STORES RT_NT_NARROW
 namespace tile16 {
 #include "rt_trace.inc"
 }  // namespace tile16
 #undef RT_TILE_W
+#undef RT_NT_STORES
 #define RT_TILE_W RT_TILE_WIDE
+#define RT_NT_STORES RT_NT_WIDE
 namespace wide {
 #include "rt_trace.inc"
 }  // namespace wide

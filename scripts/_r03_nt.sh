@@ -1,0 +1,12 @@
+#!/bin/bash
+# Round 3: nontemporal frame stores (RT_NT_STORE=1) vs plain, on the large
+# frames (wide 128x2 tiles: configs 4, 5 dense) and config 3.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out; export TMPDIR=/tmp
+V=opencl-ray-tracer_amd/variants
+L="$V/librt_hip_nt0.so $V/librt_hip_nt1.so"
+run() { n=$1; shift; timeout -k 10 200 python scripts/bench_variants.py $L --kernels "$@" > gpurun_out/nt_$n.json 2>&1 || { tail gpurun_out/nt_$n.json; exit 1; }; }
+run c3 --rounds 7
+run c4 --width 8192 --height 8192 --spheres 192 --cubes 64 --seed 4 --steps 10 --rounds 7
+run c5d --width 16384 --height 16384 --spheres 4096 --cubes 0 --seed 5 --steps 5 --rounds 5
+run c5d_rgba8 --width 16384 --height 16384 --spheres 4096 --cubes 0 --seed 5 --steps 5 --rounds 5 --format rgba8
+for f in gpurun_out/nt_*.json; do echo "== $f"; grep -v amdgpu.ids $f | tr -d '\n ' ; echo; done
