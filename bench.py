@@ -81,6 +81,8 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-path", action="store_true",
                     help="skip the end-to-end rt_render (host buffers) measurement")
+    ap.add_argument("--app-calls", type=int, default=20,
+                    help="host_path.app: warm rt_render calls per scene and format")
     ap.add_argument("--no-extras", action="store_true",
                     help="time only the headline workload (N=1: no RGBA8 Texture line; "
                          "N>1: no Texture / config 4 / weak-scaling keys)")
@@ -88,7 +90,8 @@ def parse(argv=None):
                     help="kernel path: generic = the brute-force per-pixel kernel (every ray "
                          "against every primitive), for the compute-bound comparison")
     ap.add_argument("--trace-mode", type=int, default=0,
-                    help="diagnostics ablation: 1 = stores only, 2 = no per-pixel tests")
+                    help="diagnostics ablation (needs the RT_DIAG=1 build): 1 = stores only, "
+                         "2 = no per-pixel tests")
     ap.add_argument("--pmc", default=str(REPO / "profiles" / "r03_pmc_config3.json"),
                     help="committed PMC summary to read `traffic` from")
     ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
@@ -105,11 +108,15 @@ def parse(argv=None):
     ap.add_argument("--inflight-rgba8", type=int, default=3,
                     help="the same for the texture_rgba8 leg (its trace leaves more room "
                          "beside it: 3 slots measured best, DESIGN.md §3.4)")
-    ap.add_argument("--pg-timeout", type=float, default=180.0,
-                    help="N>1: seconds before a stuck collective raises / aborts")
-    ap.add_argument("--phase-deadline", type=float, default=120.0,
-                    help="N>1: rank 0 prints the line so far and exits when one measurement "
-                         "phase runs longer than this (below --pg-timeout)")
+    ap.add_argument("--pg-timeout", type=float, default=60.0,
+                    help="N>1: seconds before a data-path collective that another rank left "
+                         "unmatched raises (gloo) or has its communicator aborted (RCCL, "
+                         "TORCH_NCCL_ASYNC_ERROR_HANDLING=2), so the phase fails and the "
+                         "later phases still run; well below --phase-deadline")
+    ap.add_argument("--phase-deadline", type=float, default=150.0,
+                    help="N>1: a phase still running after this long (a hang the collective "
+                         "timeout did not end) makes rank 0 print the line so far and every "
+                         "rank exit with status 3")
     ap.add_argument("--fail-assembly", default="",
                     help=argparse.SUPPRESS)  # tests: NAME[:RANK] raises in that assembly
     return ap.parse_args(argv)
@@ -207,6 +214,11 @@ class Ctx:
             # (Phases) prints the line before it
             timeout = datetime.timedelta(seconds=args.pg_timeout)
             if self.backend == "nccl":
+                # a collective left unmatched by a rank that failed out of a
+                # phase: after --pg-timeout the communicator is aborted and
+                # the blocked call fails (CleanUpOnly), instead of the
+                # process being torn down with the line unprinted
+                os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "2")
                 dist.init_process_group("nccl", device_id=torch.device("cuda", self.gpu),
                                         timeout=timeout)
             else:
@@ -279,23 +291,31 @@ class Ctx:
         return self.max_over_ranks(wall)
 
 
+# Exit status of an N>1 run (every rank): 0 = every phase completed and the
+# line has a value; EXIT_HUNG = a phase hung past --phase-deadline (the
+# watchdog ended the run, rank 0 printed the line first) or a rank left the
+# run; EXIT_NO_VALUE = every phase completed but no assembly was bit-exact.
+EXIT_HUNG = 3
+EXIT_NO_VALUE = 4
+
+
 class Phases:
     """The N>1 run as named phases, so one failing or hanging measurement
-    never costs the JSON line (rank 0 prints it in every case).
+    never costs the JSON line (rank 0 prints it in every case), and the exit
+    status tells a launcher what happened.
 
     run(key, fn): fn() on every rank; its value goes to target[key].  An
     exception on any rank becomes {"error": ...} under that key on every
     rank: the ranks agree over a separate gloo group (`ctrl`), so the
     agreement never pairs with a data-path collective another rank is still
-    blocked in (that rank's collective times out after --pg-timeout and it
-    joins the agreement).  A phase still running after `deadline_s` makes
-    rank 0's watchdog print the line built so far, that phase marked
-    {"error": "timeout ..."}, and end the process (os._exit(0)): the driver
-    still gets its line when an RCCL collective hangs (RCCL would abort the
-    process only later, at --pg-timeout).  The other ranks then end quietly
-    with status 0 too (their own watchdog a little later, or the agreement
-    failing once rank 0 is gone), so the launcher reports success for a run
-    whose line, errors included, was printed."""
+    blocked in (that rank's collective fails after --pg-timeout and it joins
+    the agreement); the later phases then run on a fresh data-path group.
+    A caught exception is a completed phase: the run still exits 0.
+    A phase still running after `deadline_s` is a hang: rank 0's watchdog
+    prints the line built so far, that phase marked {"error": "timeout
+    ..."}, and ends the process with EXIT_HUNG; the other ranks end with
+    EXIT_HUNG too (their own watchdog a little later, or the agreement
+    failing once rank 0 is gone)."""
 
     GRACE_S = 20.0  # non-root ranks outlive rank 0's deadline by this much
 
@@ -315,8 +335,8 @@ class Phases:
         if c.distributed or c.rank == 0:
             threading.Thread(target=self._watch, daemon=True).start()
 
-    def _quit(self, why: str):
-        """End this process with status 0 once the line is out (rank 0
+    def _quit(self, why: str, status: int = EXIT_HUNG):
+        """End this process with `status` once the line is out (rank 0
         prints it first, with the current phase marked as failed)."""
         with self.lock:
             if self.c.rank == 0 and not self.printed and self.current is not None:
@@ -324,9 +344,9 @@ class Phases:
                 target[key] = {"error": why}
             self.emit()
         sys.stdout.flush()
-        sys.stderr.write(f"bench.py rank {self.c.rank}: {why}; exiting\n")
+        sys.stderr.write(f"bench.py rank {self.c.rank}: {why}; exiting with status {status}\n")
         sys.stderr.flush()
-        os._exit(0)
+        os._exit(status)
 
     def _watch(self):
         limit = self.deadline + (0.0 if self.c.rank == 0 else self.GRACE_S)
@@ -337,7 +357,7 @@ class Phases:
                 if cur is None or self.printed or time.monotonic() - cur[2] < limit:
                     continue
             self._quit(f"timeout: phase still running after {self.deadline:.0f} s "
-                       f"(rank 0's watchdog)")
+                       f"(rank {self.c.rank}'s watchdog)")
 
     def emit(self):
         """Print the line once (rank 0).  From the watchdog thread the main
@@ -384,12 +404,17 @@ class Phases:
 
 
 def failing(args, c, name: str) -> bool:
-    """--fail-assembly NAME[:RANK] (tests): does assembly NAME raise on this
-    rank?"""
+    """--fail-assembly NAME[:RANK[:hang]] (tests): does assembly NAME raise
+    on this rank?  With ":hang" the rank hangs in it instead (a collective
+    that never completes, for the watchdog's end-to-end test)."""
     if not args.fail_assembly:
         return False
-    what, _, rank = args.fail_assembly.partition(":")
-    return what == name and (rank == "" or int(rank) == c.rank)
+    what, rank, mode = (args.fail_assembly.split(":") + ["", ""])[:3]
+    hit = what == name and (rank == "" or int(rank) == c.rank)
+    if hit and mode == "hang":
+        while True:
+            time.sleep(1.0)
+    return hit
 
 
 class HipStreams:
@@ -494,10 +519,77 @@ def frame_tensor(c: Ctx, rows, width, fmt):
 # ---------------------------------------------------------------------------
 # N = 1
 # ---------------------------------------------------------------------------
+APP_W, APP_H = 640, 480  # resources/defaultSettings.xml:1 (and Platform.cpp:264's minimum)
+
+
+def _timing_ms(t) -> dict:
+    return {"total_ms": round(t.total_us / 1e3, 4), "upload_ms": round(t.upload_us / 1e3, 4),
+            "kernel_ms": round(t.kernel_us / 1e3, 4), "download_ms": round(t.download_us / 1e3, 4)}
+
+
+def measure_app(args, c: Ctx, pkg) -> dict:
+    """SURVEY.md §8f row f4 at the app's own workload: reference scenes 1-3
+    (MainState.cpp:419-639, the golden fixtures' packed arrays) at 640x480
+    (resources/defaultSettings.xml:1), through rt_render -- the replacement
+    of executeRayTracerOpenCL, timed over the reference's timer scope
+    (MainState.cpp:662-894: scene upload, render, blocking readback) into a
+    reused, pageable host buffer like the app's `pixels` (:215).  Per scene
+    and format, on a fresh context: rt_init (openCLInit's place,
+    :1181-1326), the first call (cold) and the median of the warm calls --
+    the number that replaces the app's "Time: X ms" label (:896-904).  Every
+    frame is compared with the golden frame (RGBA8: its Texture packing,
+    :1023-1037) in the same run."""
+    import statistics
+
+    golden = REPO / "tests" / "golden"
+    res = {"scope": "rt_render: scene upload + kernels + frame download into a reused pageable "
+                    "host buffer (MainState.cpp:662-894); first call of a fresh context and "
+                    f"the median of {args.app_calls} warm calls",
+           "resolution": f"{APP_W}x{APP_H}", "scenes": {}}
+    for sid in (1, 2, 3):
+        z = np.load(golden / f"scene{sid}_{APP_W}x{APP_H}.npz")
+        scene = pkg.Scene(z["sphere_origins"], z["sphere_radius"], z["sphere_colours"],
+                          z["cube_vertices"], z["cube_colours"])
+        want32 = z["frame"]
+        ent = {"spheres": scene.num_spheres, "cubes": scene.num_cubes}
+        for fmt in ("i32x4", "rgba8"):
+            want = want32 if fmt == "i32x4" else pkg.pack_rgba8(want32)
+            out = np.empty(want.shape, want.dtype)
+            out.fill(0)  # touched once, like a reserved `pixels` vector
+            t0 = time.perf_counter()
+            rt = pkg.RayTracer(c.gpu)
+            init_ms = (time.perf_counter() - t0) * 1e3
+            try:
+                ok = True
+                _, first = rt.render(scene, APP_W, APP_H, fmt=fmt, out=out)
+                ok &= bool(np.array_equal(out, want))
+                warm = []
+                for _ in range(args.app_calls):
+                    out.fill(0)
+                    _, t = rt.render(scene, APP_W, APP_H, fmt=fmt, out=out)
+                    ok &= bool(np.array_equal(out, want))
+                    warm.append(t)
+                kernel = rt.last_kernel()
+            finally:
+                rt.close()
+            med = {key: round(statistics.median(getattr(t, key) for t in warm) / 1e3, 4)
+                   for key in ("total_us", "upload_us", "kernel_us", "download_us")}
+            ent[fmt] = {"init_ms": round(init_ms, 3), "first": _timing_ms(first),
+                        "warm_median": {k.replace("_us", "_ms"): v for k, v in med.items()},
+                        "first_over_warm_kernel": round(first.kernel_us / max(
+                            statistics.median(t.kernel_us for t in warm), 1e-9), 2),
+                        "kernel": kernel,
+                        "frame_check": "bit-exact" if ok else "MISMATCH"}
+        res["scenes"][f"scene{sid}"] = ent
+    return res
+
+
 def run_single(args, c: Ctx, pkg):
     torch = c.torch
     w, h = args.width, args.height
     k = args.k if args.k is not None else w / 640.0
+    # the app's own workload first, so its first rt_init is the process's
+    app = None if args.no_host_path else measure_app(args, c, pkg)
     scene, ds = device_scene(pkg, c, w, h, args.spheres, args.cubes, args.seed, k)
     rt = pkg.RayTracer(c.gpu)
     rt.set_trace_mode(args.trace_mode)
@@ -542,6 +634,7 @@ def run_single(args, c: Ctx, pkg):
     prof_wall_ms = c.timed(step, args.steps)
     prof = rt.profile_read()
     rt.profile(False)
+    kernel = rt.last_kernel()  # the kernel the library actually ran
     n = max(prof["renders"], 1)
     trace_ms, prep_ms, bin_ms = prof["trace_ms"] / n, prof["prep_ms"] / n, prof["bin_ms"] / n
 
@@ -576,7 +669,7 @@ def run_single(args, c: Ctx, pkg):
                     "download_ms": round(best.download_us / 1e3, 3),
                     "mrays_end_to_end": round(rays / best.total_us, 1)}
         host = {"scope": "rt_render: scene upload + kernels + frame download (PCIe) into a "
-                         "reused host buffer", **host_runs()}
+                         "reused host buffer", **host_runs(), "app": app}
         # the same into a page-locked buffer (rt_host_register): direct DMA
         pkg.host_register(host_buf)
         host["registered"] = host_runs()
@@ -631,6 +724,7 @@ def run_single(args, c: Ctx, pkg):
             tstep()
         tp = rt.profile_read()
         rt.profile(False)
+        t_kernel = rt.last_kernel()
         t_trace = tp["trace_ms"] / max(tp["renders"], 1)
         t_bytes = BYTES_PER_RAY["rgba8"] * w * h
         t_ach = t_bytes / (t_trace * 1e-3) / 1e9
@@ -643,14 +737,13 @@ def run_single(args, c: Ctx, pkg):
                                   "value": round(mrays_per_s(w * h, t_wall), 1)},
                    "roofline": {"bound": "hbm", "achieved": round(t_ach, 1), "peak": HBM_PEAK_GBS,
                                 "unit": "GB/s", "frac": round(t_ach / HBM_PEAK_GBS, 4),
-                                "kernel": kernel_name(args), "kernel_ms": round(t_trace, 4),
+                                "kernel": t_kernel, "kernel_ms": round(t_trace, 4),
                                 "algo_bytes_per_launch": t_bytes,
                                 "note": "bound by per-wave test chains, not HBM (DESIGN.md §3, profiles/r02/pmc_mix)"}}
         del tex
 
     cpu = None if args.no_cpu_baseline else cpu_baseline(args, scene, w, h)
     workload = CONFIG_NAMES.get((w, h, args.spheres, args.cubes), "custom")
-    kernel = kernel_name(args)
     rt.close()
     return {
         "metric": METRIC, "value": round(mrays_per_s(rays, value_ms), 1), "unit": "Mrays/s",
@@ -680,14 +773,6 @@ def run_single(args, c: Ctx, pkg):
         "cpu_baseline": cpu,
         "host_path": host,
     }
-
-
-def kernel_name(args) -> str:
-    """The dominant kernel: scenes of at most 512 primitives take
-    trace_small_kernel."""
-    return ("generic_kernel" if args.path == "generic" else
-            "trace_small_kernel" if 0 < args.spheres + 12 * args.cubes <= 512 else
-            "trace3_kernel")
 
 
 def cpu_baseline(args, scene, w, h):
@@ -946,40 +1031,36 @@ def calibrate_peer_store(args, c, pkg, rt, ds, width, height, fmt):
 
 def measure_host_frame(args, c: Ctx, pkg, rt, scene, w, h, fmt="i32x4"):
     """The reference's own consumer, a host frame (`pixels`, MainState.cpp:
-    215/676, read back at :876-907), filled by N GPUs at once: every rank
-    calls rt_render (the executeRayTracerOpenCL replacement: scene upload,
-    render, download -- the app's timer scope, :662-894) for its band,
-    straight into its rows of ONE page-locked host frame shared by the ranks
-    (POSIX shared memory), each over its own GPU's PCIe link.  A step ends
-    when every rank's rows are in (barrier).  Checked bit-exactly on rank 0
-    against a one-GPU device render."""
-    from multiprocessing import resource_tracker, shared_memory
+    215/676, read back at :876-907, or the Texture's RGBA8 pixels,
+    :984-994, :1023-1037), filled by N GPUs at once: every rank calls
+    rt_render (the executeRayTracerOpenCL replacement: scene upload, render,
+    download -- the app's timer scope, :662-894) for its band, straight into
+    its rows of ONE page-locked host frame shared by the ranks
+    (rowbands.HostFrame), each over its own GPU's PCIe link.  A step ends
+    when every rank's rows are in (barrier).  The same scope with rank 0
+    alone rendering the whole frame into the same buffer, in the same run,
+    gives `scaling` = t(N=1) / t(N).  Checked bit-exactly on rank 0 against
+    a one-GPU device render."""
+    from opencl_ray_tracer_amd.rowbands import HostFrame, band_rows
 
-    from opencl_ray_tracer_amd.rowbands import band_rows
-
-    shape = (h, w, 4) if fmt == "i32x4" else (h, w)
     nbytes = BYTES_PER_RAY[fmt] * w * h
     rb, re = band_rows(h, c.world, c.rank)
-    shm = frame = None
-    name = [None]
+    hf = HostFrame(h, w, fmt, c.rank, group=c.pg, register=pkg.host_register,
+                   unregister=pkg.host_unregister)
     try:
-        if c.rank == 0:
-            shm = shared_memory.SharedMemory(create=True, size=nbytes)
-            name = [shm.name]
-        c.dist.broadcast_object_list(name, 0, group=c.pg)
-        if c.rank != 0:
-            shm = shared_memory.SharedMemory(name=name[0])
-            resource_tracker.unregister(shm._name, "shared_memory")  # rank 0 unlinks it
-        frame = np.ndarray(shape, np.int32 if fmt == "i32x4" else np.uint32, buffer=shm.buf)
-        pkg.host_register(frame)
-        band = frame[rb:re]
-
         def step():
             if re > rb:
-                rt.render(scene, w, h, rows=(rb, re), fmt=fmt, out=band)
+                rt.render(scene, w, h, rows=(rb, re), fmt=fmt, out=hf.band(rb, re))
+            c.dist.barrier(group=c.pg)
+
+        def step_one():  # rank 0 alone, the whole frame, same buffer and scope
+            if c.rank == 0:
+                rt.render(scene, w, h, fmt=fmt, out=hf.frame)
             c.dist.barrier(group=c.pg)
         for _ in range(max(1, args.warmup)):
+            step_one()
             step()
+        ms1 = c.timed(step_one, args.steps)
         ms = c.timed(step, args.steps)
         ok = c.torch.ones(1, dtype=c.torch.int32, device=c.coll_dev)
         if c.rank == 0:
@@ -988,23 +1069,23 @@ def measure_host_frame(args, c: Ctx, pkg, rt, scene, w, h, fmt="i32x4"):
             rt.bind_render_device(ds, w, h, (0, h), ref.data_ptr(), fmt=fmt,
                                   stream=c.stream.cuda_stream)()
             c.sync()
-            ok.fill_(int(np.array_equal(ref.cpu().numpy().view(frame.dtype), frame)))
+            ok.fill_(int(np.array_equal(ref.cpu().numpy().view(hf.dtype), hf.frame)))
             del ref, keep
         c.dist.broadcast(ok, 0, group=c.pg)
-        pkg.host_unregister(frame)
         return {"scope": "rt_render per rank (scene upload + render + band download over its "
                          "own PCIe link) into one shared page-locked host frame, then a barrier",
                 "format": fmt, "ms_per_step": round(ms, 4),
                 "mrays_end_to_end": round(mrays_per_s(w * h, ms), 1),
                 "host_gbs": round(nbytes / (ms * 1e-3) / 1e9, 1),
+                "one_gpu": {"ms_per_step": round(ms1, 4),
+                            "mrays_end_to_end": round(mrays_per_s(w * h, ms1), 1),
+                            "scope": "rank 0 alone renders the whole frame into the same buffer "
+                                     "(same run, same scope)"},
+                "scaling": round(ms1 / ms, 3),
                 "frame_check": "bit-exact" if int(ok.item()) else "MISMATCH"}
     finally:
-        del frame
-        if shm is not None:
-            shm.close()
-            c.dist.barrier(group=c.pg)
-            if c.rank == 0:
-                shm.unlink()
+        step = step_one = None
+        hf.close()
 
 
 def device_scene_from(c: Ctx, scene):
@@ -1113,7 +1194,7 @@ def run_multi(args, c: Ctx, pkg):
     phases.run("setup", setup, state)
     if "error" in state["setup"]:
         phases.emit()
-        return
+        return EXIT_NO_VALUE
     rt, ds, scene = env["rt"], env["ds"], env["scene"]
 
     measure_assemblies(args, c, pkg, rt, ds, w, h, args.format, phases, state["assembly"],
@@ -1132,12 +1213,13 @@ def run_multi(args, c: Ctx, pkg):
             step()
         prof = rt.profile_read()
         rt.profile(False)
+        kernel = rt.last_kernel() if re > rb else None
         trace_ms = prof["trace_ms"] / max(prof["renders"], 1)
         band_bytes = BYTES_PER_RAY[args.format] * w * (re - rb)
         achieved = band_bytes / (trace_ms * 1e-3) / 1e9 if trace_ms > 0 else 0.0
         return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                "kernel": kernel_name(args), "kernel_ms": round(trace_ms, 4),
+                "kernel": kernel, "kernel_ms": round(trace_ms, 4),
                 "algo_bytes_per_launch": band_bytes, "scope": "rank 0's band, local stores"}
     phases.run("roofline", roofline, state)
 
@@ -1181,9 +1263,12 @@ def run_multi(args, c: Ctx, pkg):
                                 f"rows, no assembly",
                     "ms_per_step": round(wms, 4), "mrays": round(mrays_per_s(w * hw, wms), 1)}
         phases.run("weak_scaling", weak, state)
-        # the app's host frame filled by every GPU over its own PCIe link
-        phases.run("host_frame", lambda: measure_host_frame(args, c, pkg, rt, scene, w, h),
-                   state)
+        # the app's host frame -- `pixels` (int32x4) and the Texture (RGBA8) --
+        # filled by every GPU over its own PCIe link, beside one GPU filling it
+        state["host_frame"] = {}
+        for fmt in ("i32x4", "rgba8"):
+            phases.run(fmt, lambda fmt=fmt: measure_host_frame(args, c, pkg, rt, scene, w, h, fmt),
+                       state["host_frame"])
 
     # the CPU path beside the GPU numbers, timed on rank 0's
     # host CPUs while the other ranks wait
@@ -1192,6 +1277,15 @@ def run_multi(args, c: Ctx, pkg):
                    lambda: cpu_baseline(args, scene, w, h) if c.rank == 0 else None, state)
     rt.close()
     phases.emit()
+    return exit_status(state)
+
+
+def exit_status(state: dict) -> int:
+    """Every phase completed (a caught exception included): 0 when an
+    assembly gave the line its value, else EXIT_NO_VALUE.  Every rank holds
+    the same assembly results (frame checks are broadcast), so every rank
+    returns the same status."""
+    return 0 if pick_value(state.get("assembly", {}))[0] else EXIT_NO_VALUE
 
 
 def main():
@@ -1199,9 +1293,9 @@ def main():
     c = Ctx(args)
     pkg = __graft_entry__.load_package()
     if c.distributed:
-        run_multi(args, c, pkg)  # rank 0 prints the line
+        status = run_multi(args, c, pkg)  # rank 0 prints the line
         c.dist.destroy_process_group()
-        return
+        sys.exit(status)
     line = run_single(args, c, pkg)
     print(json.dumps(line), flush=True)
 

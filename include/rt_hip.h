@@ -51,6 +51,15 @@ enum {
     RT_PATH_GENERIC = 2  /* any origins / direction, brute force per pixel */
 };
 
+/* The kernel that did a render's per-pixel work (rt_last_kernel). */
+enum {
+    RT_KERNEL_NONE = 0,         /* no render yet */
+    RT_KERNEL_TRACE = 1,        /* prep_kernel -> coarse3_kernel -> trace3_kernel */
+    RT_KERNEL_TRACE_SMALL = 2,  /* prep_kernel -> trace_small_kernel (<= 512 primitives) */
+    RT_KERNEL_FRAME_SMALL = 3,  /* frame_small_kernel, one launch (<= 128 primitives) */
+    RT_KERNEL_GENERIC = 4       /* generic_kernel: explicit origins / any direction */
+};
+
 typedef struct rt_scene {
     const float* sphere_origins;
     const float* sphere_radius;
@@ -82,9 +91,23 @@ typedef struct rt_timing {
 typedef struct rt_ctx rt_ctx;
 
 /* Replaces MainState::openCLInit (MainState.cpp:1181-1326): selects HIP
- * device `device_ordinal`, creates the stream and the workspace.  One
- * context per device; not re-entrant per context. */
+ * device `device_ordinal` and loads every kernel's code object onto it (the
+ * counterpart of clBuildProgram / clCreateKernel, :1302-1320), so the first
+ * render pays no loading.  The stream is created on first use and the
+ * workspace grows on demand (or up front with rt_reserve).  One context per
+ * device; not re-entrant per context. */
 int rt_init(int device_ordinal, rt_ctx** out_ctx);
+
+/* Sizes the context's workspace ahead of the first render of a frame of
+ * `rows` x `width` pixels with this many spheres / cubes in `out_format`:
+ * the host-API scene copy and frame, the binned path's records and
+ * candidate lists, and the context's stream.  openCLInit does its one-time
+ * work before any trace (MainState.cpp:1290-1320, outside the trace timer
+ * :662-894); with rt_reserve the first rt_render of that size allocates
+ * nothing.  Optional: rt_render reserves what it needs itself, before its
+ * timed events.  Workspace only grows. */
+int rt_reserve(rt_ctx* ctx, int32_t width, int32_t rows, int32_t num_spheres,
+               int32_t num_cubes, int32_t out_format);
 
 /* Releases everything rt_init / rt_render allocated (MainState.cpp:73-78). */
 void rt_destroy(rt_ctx* ctx);
@@ -180,6 +203,10 @@ int rt_host_unregister(void* host_ptr);
 int rt_profile_enable(rt_ctx* ctx, int enable);
 int rt_profile_read(rt_ctx* ctx, double* prep_ms, double* bin_ms,
                     double* trace_ms, int32_t* n_renders);
+
+/* The kernel (RT_KERNEL_*) the last render enqueued on this context did
+ * its per-pixel work with (for reports: which path actually ran). */
+int rt_last_kernel(rt_ctx* ctx, int32_t* kernel);
 
 /* Device facts for reporting (HBM bytes, CU count, name). */
 int rt_device_info(rt_ctx* ctx, char* name, int32_t name_len, int32_t* n_cu,

@@ -43,11 +43,6 @@ int rt_debug_tile_shape(int32_t* w, int32_t* h);
  * wave-uniform for that row. */
 int rt_debug_block_shape(int32_t* w, int32_t* h);
 
-/* Trace-kernel ablation for measurements: 0 = the real kernel, 1 = stores
- * only, 2 = no per-pixel tests, 3 = no stores, 4 = no colour gather (a
- * constant colour).  Modes 1-4 produce wrong frames by design. */
-int rt_debug_set_trace_mode(rt_ctx* ctx, int mode);
-
 /* Byte budget for the coarse candidate lists (8 B x (primitives + 16) per
  * 64x64 bin: an id and a tile word; 20 B with RT_ROWBITS=1); binned frames
  * over it render as internal row bands.

@@ -14,6 +14,8 @@ int ctx_device(const rt_ctx* ctx);
 // the context's own stream, created on first use (nullptr if that fails):
 // a context used only with caller streams never takes a hardware queue
 hipStream_t ctx_stream(rt_ctx* ctx);
+// load rt_scene_device.hip's kernels onto the current device (rt_init)
+int preload_scene_kernels();
 }  // namespace rt_internal
 
 #endif /* RT_INTERNAL_H */

@@ -45,8 +45,13 @@ EXPORTED_SYMBOLS = (
     "rt_deg_to_rad", "rt_primary_ray_dir", "rt_scene_reference", "rt_scene_synthetic",
     "rt_pack_rgba8", "rt_abi_version", "rt_cube_build_device", "rt_scene_synthetic_device",
     "rt_render_multi", "rt_shared_alloc", "rt_shared_open", "rt_shared_close", "rt_shared_free",
-    "rt_host_register", "rt_host_unregister",
+    "rt_host_register", "rt_host_unregister", "rt_reserve", "rt_last_kernel",
 )
+# rt_last_kernel's codes (RT_KERNEL_*, rt_hip.h) by name
+KERNEL_NAMES = {0: None, 1: "trace3_kernel", 2: "trace_small_kernel", 3: "frame_small_kernel",
+                4: "generic_kernel"}
+# exported only by the diagnostics build (make RT_DIAG=1, include/rt_hip_diag.h)
+DIAG_SYMBOLS = ("rt_debug_set_trace_mode",)
 
 
 class RtError(RuntimeError):
@@ -148,6 +153,8 @@ def library() -> ctypes.CDLL:
         "rt_debug_triangle_box": (ctypes.c_int, [vp, vp, vp, vp, i32, i32, i32, vp, vp]),
         "rt_debug_sphere_box": (ctypes.c_int, [vp, f32, vp, i32, i32, i32, vp, vp]),
         "rt_debug_set_trace_mode": (ctypes.c_int, [vp, ctypes.c_int]),
+        "rt_reserve": (ctypes.c_int, [vp, i32, i32, i32, i32, i32]),
+        "rt_last_kernel": (ctypes.c_int, [vp, ctypes.POINTER(i32)]),
         "rt_debug_set_list_budget": (ctypes.c_int, [vp, ctypes.c_int64]),
         "rt_debug_set_bin_masks": (ctypes.c_int, [vp, ctypes.c_int]),
         "rt_debug_set_small_path": (ctypes.c_int, [vp, ctypes.c_int]),
@@ -166,6 +173,8 @@ def library() -> ctypes.CDLL:
         "rt_selftest_sincosf": (ctypes.c_int, [vp, vp, ctypes.c_int64, vp, vp]),
     }
     for name, (res, args) in sig.items():
+        if name in DIAG_SYMBOLS and not hasattr(lib, name):
+            continue  # the default (non-diagnostics) build
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
@@ -497,8 +506,30 @@ class RayTracer:
         return {"prep_ms": a.value, "bin_ms": b.value, "trace_ms": c.value, "renders": n.value}
 
     def set_trace_mode(self, mode: int) -> None:
-        """Diagnostics ablation of the trace kernel (0 = normal)."""
-        _check(library().rt_debug_set_trace_mode(self._ctx, mode), "rt_debug_set_trace_mode")
+        """Diagnostics ablation of the trace kernel (0 = normal).  Modes other
+        than 0 need the diagnostics build (make RT_DIAG=1); the default
+        library has only the real kernel."""
+        lib = library()
+        if not hasattr(lib, "rt_debug_set_trace_mode"):
+            if mode:
+                raise RtError(RT_ERR_UNSUPPORTED, "rt_debug_set_trace_mode (needs RT_DIAG=1)")
+            return
+        _check(lib.rt_debug_set_trace_mode(self._ctx, mode), "rt_debug_set_trace_mode")
+
+    def reserve(self, width: int, rows: int, n_spheres: int, n_cubes: int,
+                fmt: str = "i32x4") -> None:
+        """rt_reserve: size the workspace for frames of this shape ahead of
+        the first render (openCLInit's one-time setup, MainState.cpp:1290-1320)."""
+        _check(library().rt_reserve(self._ctx, width, rows, n_spheres, n_cubes, _FORMATS[fmt]),
+               "rt_reserve")
+
+    def last_kernel(self) -> Optional[str]:
+        """rt_last_kernel: the kernel the last render did its per-pixel work
+        with ("trace3_kernel", "trace_small_kernel", "frame_small_kernel",
+        "generic_kernel"; None before any render)."""
+        k = ctypes.c_int32()
+        _check(library().rt_last_kernel(self._ctx, ctypes.byref(k)), "rt_last_kernel")
+        return KERNEL_NAMES.get(k.value)
 
     def set_list_budget(self, nbytes: int) -> None:
         """Diagnostics: coarse-list byte budget (0 = default); frames over it
@@ -603,7 +634,7 @@ def debug_triangle_prep(v0, v1, v2, ray_dir, width, row_begin, row_end):
 
 def debug_triangle_prep_wide(v0, v1, v2, ray_dir, width, row_begin, row_end):
     """debug_triangle_prep of the wide-tile (128x2) build (its classifier margin
-    covers 64-pixel tile spans)."""
+    covers 128-pixel tile spans: kTileSpan = max(kWaveTile, kWaveTileH))."""
     a = [np.ascontiguousarray(v, np.float32)[:3].copy() for v in (v0, v1, v2)]
     d = np.ascontiguousarray(ray_dir, np.float32)
     box = np.zeros(4, np.int32)

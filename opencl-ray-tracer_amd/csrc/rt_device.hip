@@ -42,11 +42,23 @@
 #include <thread>
 #include <vector>
 
+#include "rt_args.h"
 #include "rt_hip.h"
 #include "rt_hip_debug.h"
+#include "rt_hip_diag.h"
 #include "rt_internal.h"
 
 #pragma clang fp contract(off)
+
+// Diagnostics build (make RT_DIAG=1): the trace-kernel ablations of
+// rt_debug_set_trace_mode (rt_hip_diag.h) and the RT_TIMELINE / RT_SKIP_DIAG
+// instrumentation.  The default library instantiates and exports none of it.
+#ifndef RT_DIAG
+#define RT_DIAG 0
+#endif
+#if !RT_DIAG && ((defined(RT_TIMELINE) && RT_TIMELINE) || (defined(RT_SKIP_DIAG) && RT_SKIP_DIAG))
+#error "RT_TIMELINE and RT_SKIP_DIAG are diagnostics: build with RT_DIAG=1"
+#endif
 
 #ifndef RT_BIN_MASKS
 #define RT_BIN_MASKS 1            // default of rt_debug_set_bin_masks
@@ -89,7 +101,8 @@ struct rt_ctx {
     unsigned* flag = nullptr;   // non-finite scene flag (generation-stamped)
     unsigned gen = 0;
     unsigned od_launches = 0;  // binned launches: picks the box-overdraw slot
-    int trace_mode = 0;  // diagnostics ablation, see trace3_kernel
+    int trace_mode = 0;  // diagnostics ablation (RT_DIAG builds), see trace3_kernel
+    int last_kernel = RT_KERNEL_NONE;  // the dominant kernel of the last launch (rt_last_kernel)
     int tile_variant = 0;  // 0 = by frame size, 1 = 16x16 tiles, 2 = the wide (128x2) tiles
     // coarse lists take 4 B x kListStride x (primitives + 16) per 64x64 bin; a frame whose
     // lists would exceed this is rendered as internal row bands
@@ -155,20 +168,7 @@ bool binned_ok(const float d[4], const float* origins) {
            std::isfinite(d[2]) && std::isfinite(d[3]);
 }
 
-int check_args(const rt_scene* s, int32_t width, int32_t height, int32_t row_begin,
-               int32_t row_end, int32_t fmt) {
-    if (!s || width <= 0 || height <= 0 || row_begin < 0 || row_end > height ||
-        row_begin >= row_end)
-        return RT_ERR_INVALID_ARG;
-    if (width > (1 << 24) || height > (1 << 24)) return RT_ERR_INVALID_ARG;  // exact float coords
-    if (s->num_spheres < 0 || s->num_cubes < 0 || s->num_lights < 0) return RT_ERR_INVALID_ARG;
-    if (s->num_spheres > 0 && (!s->sphere_origins || !s->sphere_radius || !s->sphere_colours))
-        return RT_ERR_INVALID_ARG;
-    if (s->num_cubes > 0 && (!s->cube_vertices || !s->cube_colours)) return RT_ERR_INVALID_ARG;
-    if ((int64_t)12 * s->num_cubes + s->num_spheres > (int64_t)1 << 30) return RT_ERR_INVALID_ARG;
-    if (fmt != RT_FORMAT_I32X4 && fmt != RT_FORMAT_RGBA8) return RT_ERR_INVALID_ARG;
-    return RT_OK;
-}
+using rt_args::check_args;
 
 #define HIP_TRY(x)                                    \
     do {                                              \
@@ -266,17 +266,35 @@ __global__ void __launch_bounds__(256) grid_check_kernel(const float4* __restric
 constexpr int64_t kWideTileBytes = (int64_t)1 << 29;
 
 // rt_debug_set_tile_variant: 0 = by frame size, 1 = 16x16, 2 = wide (128x2)
+bool use_wide_tiles(const rt_ctx* ctx, int32_t width, int32_t rows, int32_t fmt) {
+    const int64_t bytes = (int64_t)width * rows * (fmt == RT_FORMAT_I32X4 ? 16 : 4);
+    return ctx->tile_variant == 2 || (ctx->tile_variant == 0 && bytes >= kWideTileBytes);
+}
+
 int render_launch(rt_ctx* ctx, const rt_scene* s, const float d[4], const float* origins,
                   int32_t width, int32_t row_begin, int32_t row_end, int32_t fmt, int32_t path,
                   void* out, hipStream_t stream, int32_t* used_path) {
-    const int64_t bytes =
-        (int64_t)width * (row_end - row_begin) * (fmt == RT_FORMAT_I32X4 ? 16 : 4);
-    const bool use_wide =
-        ctx->tile_variant == 2 || (ctx->tile_variant == 0 && bytes >= kWideTileBytes);
-    return use_wide ? wide::launch(ctx, s, d, origins, width, row_begin, row_end, fmt, path, out,
-                                 stream, used_path)
-                : tile16::launch(ctx, s, d, origins, width, row_begin, row_end, fmt, path, out,
-                                 stream, used_path);
+    return use_wide_tiles(ctx, width, row_end - row_begin, fmt)
+               ? wide::launch(ctx, s, d, origins, width, row_begin, row_end, fmt, path, out,
+                              stream, used_path)
+               : tile16::launch(ctx, s, d, origins, width, row_begin, row_end, fmt, path, out,
+                                stream, used_path);
+}
+
+// The binned path's workspace for a frame of `rows` rows, in the build
+// render_launch() will pick (rt_reserve; rt_render before its first event).
+int reserve_launch(rt_ctx* ctx, int32_t width, int32_t rows, int32_t ns, int32_t nc,
+                   int32_t fmt) {
+    return use_wide_tiles(ctx, width, rows, fmt) ? wide::reserve(ctx, ns, nc, width, rows)
+                                                 : tile16::reserve(ctx, ns, nc, width, rows);
+}
+
+// rt_render's own buffers: the scene copy and the frame it downloads from.
+int reserve_host(rt_ctx* ctx, int32_t width, int32_t rows, int32_t ns, int32_t nc,
+                 int32_t fmt) {
+    int rc = ensure(&ctx->scene_buf, &ctx->scene_cap, rt_args::scene_layout(ns, nc).bytes);
+    if (rc) return rc;
+    return ensure(&ctx->out_buf, &ctx->out_cap, rt_args::frame_bytes(width, rows, fmt));
 }
 
 // the host-side restatements the debug hooks expose are the 16x16 build's
@@ -326,7 +344,38 @@ int rt_init(int device_ordinal, rt_ctx** out_ctx) {
         rt_destroy(ctx);
         return RT_ERR_OUT_OF_MEMORY;
     }
+    // One-time setup here, as openCLInit builds the program before any trace
+    // (MainState.cpp:1290-1320, outside the per-trace timer :662-894): every
+    // kernel's code object is loaded onto the device now, not inside the
+    // first render.
+    hipFuncAttributes fa;
+    if (tile16::preload() != RT_OK || wide::preload() != RT_OK ||
+        rt_internal::preload_scene_kernels() != RT_OK ||
+        hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(grid_check_kernel)) !=
+            hipSuccess) {
+        rt_destroy(ctx);
+        return RT_ERR_HIP;
+    }
     *out_ctx = ctx;
+    return RT_OK;
+}
+
+int rt_reserve(rt_ctx* ctx, int32_t width, int32_t rows, int32_t num_spheres, int32_t num_cubes,
+               int32_t out_format) {
+    if (!ctx || rt_args::check_reserve(width, rows, num_spheres, num_cubes, out_format))
+        return RT_ERR_INVALID_ARG;
+    HIP_TRY(hipSetDevice(ctx->device));
+    int rc = reserve_host(ctx, width, rows, num_spheres, num_cubes, out_format);
+    if (rc) return rc;
+    rc = reserve_launch(ctx, width, rows, num_spheres, num_cubes, out_format);
+    if (rc) return rc;
+    // the host API's stream (its hardware queue is set up on first use)
+    return rt_internal::ctx_stream(ctx) ? RT_OK : RT_ERR_HIP;
+}
+
+int rt_last_kernel(rt_ctx* ctx, int32_t* kernel) {
+    if (!ctx || !kernel) return RT_ERR_INVALID_ARG;
+    *kernel = ctx->last_kernel;
     return RT_OK;
 }
 
@@ -357,15 +406,20 @@ int rt_render_path(rt_ctx* ctx, const rt_scene* scene, const float ray_dir[4],
     const int32_t rows = row_end - row_begin;
     const size_t ns = (size_t)scene->num_spheres, nc = (size_t)scene->num_cubes;
     // one device copy of the flattened scene (MainState.cpp:666-743, 759-838)
-    const size_t o_so = 0, o_sr = align_up(16 * ns, 256), o_sc = o_sr + align_up(4 * ns, 256),
-                 o_cv = o_sc + align_up(16 * ns, 256), o_cc = o_cv + align_up(16 * 36 * nc, 256),
-                 scene_bytes = o_cc + align_up(16 * nc, 256) + 256;
-    rc = ensure(&ctx->scene_buf, &ctx->scene_cap, scene_bytes);
+    // and the frame; then the binned path's workspace, all before the first
+    // event, so that kernel_us times kernels and never an allocation (the
+    // buffers only grow: a steady-state render allocates nothing)
+    const rt_args::SceneLayout lay = rt_args::scene_layout(scene->num_spheres, scene->num_cubes);
+    rc = reserve_host(ctx, width, rows, scene->num_spheres, scene->num_cubes, out_format);
     if (rc) return rc;
+    if (path != RT_PATH_GENERIC && binned_ok(ray_dir, nullptr)) {
+        rc = reserve_launch(ctx, width, rows, scene->num_spheres, scene->num_cubes, out_format);
+        if (rc) return rc;
+    }
+    const size_t o_so = lay.sphere_origins, o_sr = lay.sphere_radius, o_sc = lay.sphere_colours,
+                 o_cv = lay.cube_vertices, o_cc = lay.cube_colours;
     const size_t px = (size_t)width * rows;
-    const size_t out_bytes = px * (out_format == RT_FORMAT_I32X4 ? 16 : 4);
-    rc = ensure(&ctx->out_buf, &ctx->out_cap, out_bytes);
-    if (rc) return rc;
+    const size_t out_bytes = rt_args::frame_bytes(width, rows, out_format);
     char* sb = static_cast<char*>(ctx->scene_buf);
     hipStream_t st = rt_internal::ctx_stream(ctx);
     if (!st) return RT_ERR_HIP;
@@ -386,7 +440,7 @@ int rt_render_path(rt_ctx* ctx, const rt_scene* scene, const float ray_dir[4],
         const size_t ob = px * 16;
         rc = ensure(&ctx->origin_buf, &ctx->origin_cap, ob);
         if (rc) return rc;
-        HIP_TRY(hipMemcpyAsync(ctx->origin_buf, ray_origins + (size_t)4 * width * row_begin, ob,
+        HIP_TRY(hipMemcpyAsync(ctx->origin_buf, rt_args::band_origins(ray_origins, width, row_begin), ob,
                                hipMemcpyHostToDevice, st));
         d_origins = static_cast<const float*>(ctx->origin_buf);
         if (path != RT_PATH_GENERIC && binned_ok(ray_dir, nullptr)) {
@@ -490,8 +544,7 @@ int rt_render_device(rt_ctx* ctx, const rt_scene* device_scene, const float ray_
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : rt_internal::ctx_stream(ctx);
     if (!st) return RT_ERR_HIP;
     // launch() reads origins from the band's first row
-    const float* band_origins =
-        device_ray_origins ? device_ray_origins + (size_t)4 * width * row_begin : nullptr;
+    const float* band_origins = rt_args::band_origins(device_ray_origins, width, row_begin);
     return render_launch(ctx, device_scene, ray_dir, band_origins, width, row_begin, row_end,
                   out_format, path, device_out, st, nullptr);
 }
@@ -638,7 +691,6 @@ int rt_debug_triangle_box(const float v0[3], const float v1[3], const float v2[3
     return ok ? 1 : 0;
 }
 
-// Diagnostics: select a trace-kernel ablation (0 = normal).
 int rt_debug_set_list_budget(rt_ctx* ctx, int64_t bytes) {
     if (!ctx || bytes < 0) return RT_ERR_INVALID_ARG;
     ctx->list_budget = bytes ? bytes : (int64_t)4 << 30;
@@ -730,11 +782,14 @@ int rt_debug_set_small_path(rt_ctx* ctx, int enable) {
     return RT_OK;
 }
 
+#if RT_DIAG
+// Diagnostics build only (rt_hip_diag.h): select a trace-kernel ablation.
 int rt_debug_set_trace_mode(rt_ctx* ctx, int mode) {
     if (!ctx || mode < 0 || mode > 4) return RT_ERR_INVALID_ARG;
     ctx->trace_mode = mode;
     return RT_OK;
 }
+#endif
 
 #if RT_TIMELINE
 // Diagnostics build only: per-wave timeline buffer (8 x uint32 per wave).

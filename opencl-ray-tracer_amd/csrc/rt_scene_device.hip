@@ -358,6 +358,18 @@ __global__ void sincosf_selftest_kernel(const float* in, int64_t n, float* s, fl
 
 }  // namespace
 
+namespace rt_internal {
+// rt_init: load this translation unit's code object now (see preload() in
+// rt_trace.inc)
+int preload_scene_kernels() {
+    hipFuncAttributes a;
+    for (const void* k : {reinterpret_cast<const void*>(cube_build_kernel),
+                          reinterpret_cast<const void*>(synthetic_scene_kernel)})
+        if (hipFuncGetAttributes(&a, k) != hipSuccess) return RT_ERR_HIP;
+    return RT_OK;
+}
+}  // namespace rt_internal
+
 extern "C" {
 
 int rt_cube_build_device(rt_ctx* ctx, const rt_cube_op* device_ops,

@@ -212,6 +212,64 @@ class SharedFrame:
         self.ptr = 0
 
 
+class HostFrame:
+    """One host frame shared by the ranks of a node: the app's own consumer
+    buffer -- `pixels` (int32x4, MainState.cpp:215, read back at :876-907)
+    or the Texture's RGBA8 surface pixels (uint32, :984-994, :1023-1037) --
+    in POSIX shared memory, so every rank's band lands in it straight over
+    its own GPU's PCIe link and no rank-to-rank copy exists.
+
+    The root creates the segment and broadcasts its name (`group`'s
+    broadcast_object_list); every rank maps it and takes `band(rb, re)`, a
+    view of its rows.  `register` / `unregister` (e.g. rt_host_register)
+    page-lock the mapping on each rank for direct DMA.  close(): every rank
+    unmaps, then (after a barrier) the root unlinks."""
+
+    def __init__(self, height: int, width: int, fmt: str, rank: int, root: int = 0,
+                 group=None, register=None, unregister=None):
+        import numpy as np
+        import torch.distributed as dist
+        from multiprocessing import resource_tracker, shared_memory
+
+        self.rank, self.root, self.group = rank, root, group
+        self.shape = (height, width, 4) if fmt == "i32x4" else (height, width)
+        self.dtype = np.int32 if fmt == "i32x4" else np.uint32
+        nbytes = int(np.prod(self.shape)) * 4
+        self.unregister = unregister
+        self.shm = None
+        self.frame = None
+        name = [None]
+        if rank == root:
+            self.shm = shared_memory.SharedMemory(create=True, size=nbytes)
+            name = [self.shm.name]
+        dist.broadcast_object_list(name, root, group=group)
+        if rank != root:
+            self.shm = shared_memory.SharedMemory(name=name[0])
+            resource_tracker.unregister(self.shm._name, "shared_memory")  # the root unlinks it
+        self.frame = np.ndarray(self.shape, self.dtype, buffer=self.shm.buf)
+        self.registered = False
+        if register is not None:
+            register(self.frame)
+            self.registered = True
+
+    def band(self, row_begin: int, row_end: int):
+        return self.frame[row_begin:row_end]
+
+    def close(self) -> None:
+        import torch.distributed as dist
+
+        if self.registered and self.unregister is not None:
+            self.unregister(self.frame)
+            self.registered = False
+        self.frame = None
+        if self.shm is not None:
+            self.shm.close()
+            dist.barrier(group=self.group)
+            if self.rank == self.root:
+                self.shm.unlink()
+            self.shm = None
+
+
 def interleaved_blocks(height: int, world: int, rank: int, block: int = 64) -> List[Tuple[int, int]]:
     """Row blocks of `block` rows dealt round-robin over the ranks (SURVEY.md
     §8e: for scenes whose load is not uniform down the frame).  64 rows is

@@ -343,8 +343,8 @@ print("not reached")
 
 def test_phase_watchdog_prints_line():
     """A phase that hangs (an RCCL collective that never completes) makes rank
-    0 print the line built so far, that phase marked as a timeout, and exit 0
-    long before the hang ends."""
+    0 print the line built so far, that phase marked as a timeout, and exit
+    with EXIT_HUNG (non-zero) long before the hang ends."""
     import json
     import subprocess
     import time
@@ -352,7 +352,7 @@ def test_phase_watchdog_prints_line():
     code = _WATCHDOG.format(repo=str(REPO), bench=str(REPO / "bench.py"))
     t0 = time.monotonic()
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=50)
-    assert r.returncode == 0, r.stderr
+    assert r.returncode == 3, (r.returncode, r.stderr)
     assert time.monotonic() - t0 < 40
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1 and "not reached" not in r.stdout
@@ -387,12 +387,13 @@ print("not reached")
 """
 
 
-def test_phase_timeout_every_rank_exits_zero(tmp_path):
+def test_phase_hang_every_rank_exits_nonzero(tmp_path):
     """An exception on rank 1 while rank 0 blocks in that phase's data-path
-    collective (an RCCL collective cannot time out and recover): rank 0's
-    watchdog prints the line with the phase marked as failed and exits 0,
-    and rank 1, waiting in the agreement, ends with status 0 as well, so the
-    launcher sees a successful run whose line carries the error."""
+    collective, whose timeout (120 s here) is beyond the phase deadline, so
+    it is a hang: rank 0's watchdog prints the line with the phase marked as
+    failed and exits with EXIT_HUNG, and rank 1, waiting in the agreement,
+    ends with EXIT_HUNG as well -- the launcher sees a failed run, and the
+    line that names the phase."""
     import json
     import subprocess
     import time
@@ -409,10 +410,94 @@ def test_phase_timeout_every_rank_exits_zero(tmp_path):
     outs = [p.communicate(timeout=100) for p in procs]
     assert time.monotonic() - t0 < 90
     for p, (out, err) in zip(procs, outs):
-        assert p.returncode == 0, err[-2000:]
+        assert p.returncode == 3, (p.returncode, err[-2000:])
         assert "not reached" not in out
     lines = [l for l in outs[0][0].splitlines() if l.startswith("{")]
     assert len(lines) == 1 and not [l for l in outs[1][0].splitlines() if l.startswith("{")]
     line = json.loads(lines[0])
     assert "error" in line["assembly"]["xgmi_peer_store"]
     assert line["ms_per_step"] == 0.25 and line["phase_errors"] == ["assembly.xgmi_peer_store"]
+
+
+_DEFAULTS = r"""
+import datetime, os, sys, time
+sys.path.insert(0, {repo!r})
+sys.argv = ["bench.py"]
+import importlib.util
+spec = importlib.util.spec_from_file_location("rt_bench", {bench!r})
+b = importlib.util.module_from_spec(spec); spec.loader.exec_module(b)
+import torch, torch.distributed as dist
+rank = int(os.environ["RANK"])
+args = b.parse(["--gpus", "2"])  # the default timeouts
+pg = datetime.timedelta(seconds=args.pg_timeout)
+dist.init_process_group("gloo", timeout=pg)
+class C:
+    world, distributed, pg = 2, True, None
+    def renew_group(self):
+        self.pg = dist.new_group(backend="gloo", timeout=pg)
+c = C()
+c.rank, c.torch, c.dist = rank, torch, dist
+state = {{"assembly": {{"rccl_p2p": {{"ms_per_step": 0.25, "frame_check": "bit-exact"}}}}}}
+ph = b.Phases(c, args.phase_deadline, lambda: b.multi_line(args, c, state), args.pg_timeout)
+t0 = time.monotonic()
+def one_rank():
+    if rank == 1:
+        raise RuntimeError("rank 1 only")
+    dist.barrier(group=c.pg)  # unmatched: fails after --pg-timeout
+ph.run("xgmi_peer_store", one_rank, state["assembly"])
+def later():
+    t = torch.ones(1)
+    dist.all_reduce(t, group=c.pg)  # the renewed group lines up again
+    return {{"ms_per_step": 0.5, "frame_check": "bit-exact", "sum": float(t.item())}}
+ph.run("xgmi_peer_store_balanced", later, state["assembly"])
+ph.run("roofline", lambda: {{"frac": 0.5, "after_s": round(time.monotonic() - t0, 1)}}, state)
+ph.emit()
+dist.destroy_process_group()
+sys.exit(b.exit_status(state))
+"""
+
+
+def test_one_rank_failure_recovers_at_default_timeouts(tmp_path):
+    """at the DEFAULT --pg-timeout / --phase-deadline, a phase
+    that fails on one rank while the other blocks in its collective ends by
+    the collective's timeout, before the watchdog: the failure is recorded,
+    the later phases (xgmi_peer_store_balanced, roofline) still run, and
+    every rank exits 0 (every phase completed, the line has a value)."""
+    import json
+    import subprocess
+    import time
+
+    b = _bench()
+    a = b.parse(["--gpus", "2"])
+    # the collective must give up well before the watchdog would fire
+    assert a.pg_timeout + 30 <= a.phase_deadline
+    code = _DEFAULTS.format(repo=str(REPO), bench=str(REPO / "bench.py"))
+    port = _free_port()
+    procs = []
+    t0 = time.monotonic()
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK=str(r),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-c", code], stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True, env=env, cwd=tmp_path))
+    outs = [p.communicate(timeout=a.phase_deadline + 60) for p in procs]
+    assert time.monotonic() - t0 < a.phase_deadline  # no watchdog involved
+    for p, (out, err) in zip(procs, outs):
+        assert p.returncode == 0, (p.returncode, err[-2000:])
+    lines = [l for l in outs[0][0].splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    line = json.loads(lines[0])
+    assert "error" in line["assembly"]["xgmi_peer_store"]  # rank 0 records its timeout
+    assert line["assembly"]["xgmi_peer_store_balanced"]["sum"] == 2.0
+    assert line["roofline"]["frac"] == 0.5
+    assert line["phase_errors"] == ["assembly.xgmi_peer_store"]
+
+
+def test_exit_status():
+    b = _bench()
+    ok = {"assembly": {"rccl_p2p": {"ms_per_step": 0.5, "frame_check": "bit-exact"},
+                       "xgmi_peer_store": {"error": "rank 1: boom"}}}
+    assert b.exit_status(ok) == 0  # a caught exception is a completed phase
+    bad = {"assembly": {"rccl_p2p": {"ms_per_step": 0.5, "frame_check": "MISMATCH"}}}
+    assert b.exit_status(bad) == b.EXIT_NO_VALUE != 0
+    assert b.exit_status({}) == b.EXIT_NO_VALUE

@@ -10,6 +10,7 @@ import pytest
 REPO = Path(__file__).resolve().parents[1]
 HEADER = REPO / "include" / "rt_hip.h"
 DEBUG_HEADER = REPO / "include" / "rt_hip_debug.h"
+DIAG_HEADER = REPO / "include" / "rt_hip_diag.h"
 
 
 def declared_functions(header=HEADER):
@@ -32,6 +33,18 @@ def test_library_exports_every_declared_symbol(pkg):
     assert set(declared_functions()) == set(pkg.EXPORTED_SYMBOLS)
     hooks = declared_functions(DEBUG_HEADER)
     assert hooks and not [n for n in hooks if not hasattr(lib, n)]
+
+
+def test_default_build_has_no_diagnostics(pkg):
+    """The shipped library (RT_DIAG=0) exports none of the diagnostics
+    build's hooks (include/rt_hip_diag.h) and instantiates no ablation
+    variant of the trace kernel: only trace3_kernel<0, format>."""
+    lib = ctypes.CDLL(str(pkg.library_path()))
+    diag = declared_functions(DIAG_HEADER)
+    assert "rt_debug_set_trace_mode" in diag
+    assert not [n for n in diag if hasattr(lib, n)]
+    names = set(re.findall(rb"trace3_kernelILi(\d)ELi(\d)E", pkg.library_path().read_bytes()))
+    assert names == {(b"0", b"0"), (b"0", b"1")}, names
 
 
 def test_abi_version(pkg):
@@ -57,6 +70,9 @@ def test_argument_validation_without_gpu(pkg):
     assert lib.rt_render_device(None, ctypes.byref(c), d.ctypes.data, None, 2, 2, 0, 2, 0, 0,
                                 out.ctypes.data, None) == pkg.RT_ERR_INVALID_ARG
     assert lib.rt_init(0, None) == pkg.RT_ERR_INVALID_ARG
+    assert lib.rt_reserve(None, 640, 480, 1, 1, 0) == pkg.RT_ERR_INVALID_ARG
+    k = ctypes.c_int32()
+    assert lib.rt_last_kernel(None, ctypes.byref(k)) == pkg.RT_ERR_INVALID_ARG
     # rt_render_multi: no contexts / a NULL context
     ctxs = (ctypes.c_void_p * 2)(None, None)
     assert lib.rt_render_multi(None, 1, ctypes.byref(c), d.ctypes.data, None, 2, 2, 0, 2, 0,

@@ -100,3 +100,63 @@ def test_interleaved_blocks_partition():
             assert rows == list(range(h))
             for rank in range(world):
                 assert all(s % 64 == 0 for s, _ in interleaved_blocks(h, world, rank))
+
+
+def _host_frame_worker(rank, world, port, width, height, fmt, result_path):
+    """Each rank renders its band (the oracle stands in for rt_render) into
+    its rows of one shared host frame (rowbands.HostFrame, what bench.py's
+    host_frame fills over every GPU's own PCIe link); rank 0 saves it."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, str(REPO))
+    sys.path.insert(0, str(REPO / "tests"))
+    import torch.distributed as dist
+
+    import __graft_entry__
+    from oracle_lib import Oracle
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        pkg = __graft_entry__.load_package()
+        from opencl_ray_tracer_amd import rowbands
+
+        oracle = Oracle()
+        scene = oracle.scene_reference(3, 1)
+        hf = rowbands.HostFrame(height, width, fmt, rank)
+        if rank == 0:
+            hf.frame[...] = 0x5A5A5A5A  # poison: every row must be overwritten
+        dist.barrier()
+        rb, re = rowbands.band_rows(height, world, rank) if height >= world else \
+            (min(rank, height), min(rank + 1, height))
+        if re > rb:
+            band = oracle.trace(scene, width, height, rows=(rb, re))
+            hf.band(rb, re)[...] = band if fmt == "i32x4" else pkg.pack_rgba8(band)
+        dist.barrier()  # every band is in
+        if rank == 0:
+            np.save(result_path, hf.frame.copy())
+        hf.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fmt,world,height", [("rgba8", 2, 97), ("i32x4", 2, 97),
+                                              ("rgba8", 3, 64), ("rgba8", 3, 2)])
+def test_host_frame_assembly_gloo(tmp_path, oracle, fmt, world, height):
+    """bench.py's host_frame: N ranks fill one shared host frame, the app's
+    `pixels` (int32x4) or its Texture's RGBA8 pixels (MainState.cpp:984-994,
+    :1023-1037), each writing only its own rows; rank 0 sees the whole
+    frame, equal to the oracle's (packed for RGBA8)."""
+    import torch.multiprocessing as mp
+
+    sys.path.insert(0, str(REPO))
+    import __graft_entry__
+    pkg = __graft_entry__.load_package()
+    width = 96
+    out = tmp_path / "frame.npy"
+    mp.spawn(_host_frame_worker, args=(world, _free_port(), width, height, fmt, str(out)),
+             nprocs=world, join=True)
+    frame = np.load(out)
+    want = oracle.trace(oracle.scene_reference(3, 1), width, height)
+    if fmt == "rgba8":
+        want = pkg.pack_rgba8(want)
+        assert frame.dtype == np.uint32 and frame.shape == (height, width)
+    assert np.array_equal(frame, want)

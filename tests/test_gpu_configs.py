@@ -172,7 +172,13 @@ def test_bench_rehearsal_assemblies(world, tmp_path):
         assert line["assembly"][how]["frame_check"] == "bit-exact", line["assembly"]
         assert line["texture_rgba8"][how]["frame_check"] == "bit-exact"
         assert line["config4"][how]["frame_check"] == "bit-exact"
-    assert line["host_frame"]["frame_check"] == "bit-exact", line["host_frame"]
+    # the app's host frame in both formats (`pixels`, the Texture), N ranks
+    # and one GPU in the same run, with the ratio
+    for fmt in ("i32x4", "rgba8"):
+        hf = line["host_frame"][fmt]
+        assert hf["frame_check"] == "bit-exact" and hf["format"] == fmt, hf
+        assert hf["scaling"] == pytest.approx(hf["one_gpu"]["ms_per_step"] / hf["ms_per_step"],
+                                              rel=2e-2)
     bal = line["assembly"]["xgmi_peer_store_balanced"]
     assert bal["frame_check"] == "bit-exact" and sum(bal["rows_per_rank"]) == 512, bal
     assert line["value"] == pytest.approx(1024 * 512 / (line["ms_per_step"] * 1e-3) / 1e6,
@@ -195,7 +201,7 @@ def test_bench_rehearsal_forced_failure(tmp_path):
            "--no-cpu-baseline", "--pg-timeout", "15", "--fail-assembly", "rccl_p2p:1"]
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=tmp_path)
-    assert p.returncode == 0, p.stderr[-3000:]
+    assert p.returncode == 0, p.stderr[-3000:]  # a caught exception: every phase completed
     lines = [s for s in p.stdout.splitlines() if s.startswith("{")]
     assert len(lines) == 1, p.stdout[-2000:]
     line = json.loads(lines[0])
@@ -205,6 +211,28 @@ def test_bench_rehearsal_forced_failure(tmp_path):
     assert line["value"] and line["config"]["parallelism"].endswith(
         ("xgmi_peer_store (rehearsal: shared cuda:0, gloo)",
          "xgmi_peer_store_balanced (rehearsal: shared cuda:0, gloo)"))
+
+
+def test_bench_rehearsal_forced_hang(tmp_path):
+    """bench.py at N>1 with one rank hanging inside an assembly (past the
+    phase deadline, the data-path timeout longer): rank 0's watchdog prints
+    exactly one line, the hung phase named in phase_errors, and the launcher
+    gets a non-zero status -- a hang is never reported as success."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node=2", "--master-addr=127.0.0.1", "--master-port=29535",
+           str(REPO / "bench.py"), "--gpus", "2", "--rehearse", "--steps", "3",
+           "--warmup", "1", "--width", "1024", "--height", "512", "--no-extras",
+           "--no-cpu-baseline", "--pg-timeout", "300", "--phase-deadline", "20",
+           "--fail-assembly", "xgmi_peer_store:1:hang"]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=110, env=env, cwd=tmp_path)
+    assert p.returncode != 0, p.stderr[-3000:]
+    lines = [s for s in p.stdout.splitlines() if s.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    line = json.loads(lines[0])
+    assert "timeout" in line["assembly"]["xgmi_peer_store"]["error"]
+    assert line["phase_errors"] == ["assembly.xgmi_peer_store"]
+    assert line["assembly"]["rccl_p2p"]["frame_check"] == "bit-exact"  # the phase before
 
 
 def _tie_scene(pkg, w, h, n, seed):
