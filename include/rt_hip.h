@@ -101,11 +101,13 @@ int rt_init(int device_ordinal, rt_ctx** out_ctx);
 /* Sizes the context's workspace ahead of the first render of a frame of
  * `rows` x `width` pixels with this many spheres / cubes in `out_format`:
  * the host-API scene copy and frame, the binned path's records and
- * candidate lists, and the context's stream.  openCLInit does its one-time
- * work before any trace (MainState.cpp:1290-1320, outside the trace timer
- * :662-894); with rt_reserve the first rt_render of that size allocates
- * nothing.  Optional: rt_render reserves what it needs itself, before its
- * timed events.  Workspace only grows. */
+ * candidate lists, and the context's stream, on which it runs one small
+ * pageable upload and download (the HIP runtime's one-time staging setup).
+ * Synchronous.  openCLInit does its one-time work before any trace
+ * (MainState.cpp:1290-1320, outside the trace timer :662-894); after
+ * rt_reserve the first rt_render of that size allocates nothing and pays no
+ * setup.  Optional: rt_render reserves what it needs itself (before its
+ * timed events).  Workspace only grows. */
 int rt_reserve(rt_ctx* ctx, int32_t width, int32_t rows, int32_t num_spheres,
                int32_t num_cubes, int32_t out_format);
 

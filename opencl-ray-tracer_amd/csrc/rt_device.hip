@@ -125,6 +125,9 @@ struct rt_ctx {
     unsigned coarse_cull_overdraw = RT_COARSE_CULL_OVERDRAW;
     unsigned coarse_cull_overdraw_rgba8 = RT_COARSE_CULL_OVERDRAW_RGBA8;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    // rt_render's kernel span: ev[1] / ev[2] ride on the first / last kernel
+    // of the render (set only while rt_render_path enqueues it)
+    hipEvent_t span_start = nullptr, span_stop = nullptr;
     // profiling: per render, start/stop events of the prep, coarse and trace
     // kernels, attached to the kernels' own dispatch packets
     bool profile = false;
@@ -170,22 +173,40 @@ bool binned_ok(const float d[4], const float* origins) {
 
 using rt_args::check_args;
 
+struct KEv {
+    hipEvent_t start, stop;
+};
+
 #define HIP_TRY(x)                                    \
     do {                                              \
         if ((x) != hipSuccess) return RT_ERR_HIP;     \
     } while (0)
 
-// Launch `kernel` on `stream`; with profiling events, through
-// hipExtLaunchKernelGGL so the start/stop timestamps are the kernel's own
-// (no extra queue packets between the kernels).
+// Launch `kernel` on `stream`; with events, through hipExtLaunchKernelGGL so
+// the start / stop timestamps are the kernel's own (no extra queue packets
+// between the kernels).  Either event may be null.
 template <typename K, typename... A>
-int launch_k(K kernel, dim3 grid, dim3 block, hipStream_t stream, const hipEvent_t* ev,
-             A... args) {
-    if (ev)
-        hipExtLaunchKernelGGL(kernel, grid, block, 0, stream, ev[0], ev[1], 0, args...);
+int launch_k(K kernel, dim3 grid, dim3 block, hipStream_t stream, KEv ev, A... args) {
+    if (ev.start || ev.stop)
+        hipExtLaunchKernelGGL(kernel, grid, block, 0, stream, ev.start, ev.stop, 0, args...);
     else
         kernel<<<grid, block, 0, stream>>>(args...);
     return hipGetLastError() == hipSuccess ? RT_OK : RT_ERR_HIP;
+}
+
+// The events one kernel of a render carries: its profiling pair (`pe`,
+// rt_profile_enable), else the render's span -- rt_render's kernel_us is
+// the first kernel's start to the last kernel's end, the kernels' own
+// timestamps, so host enqueue gaps in front of them are not kernel time.
+// The span's start is taken once (the first kernel of the first band).
+KEv kernel_events(rt_ctx* ctx, const hipEvent_t* pe, bool first, bool last) {
+    if (pe) return KEv{pe[0], pe[1]};
+    KEv e{nullptr, last ? ctx->span_stop : nullptr};
+    if (first) {
+        e.start = ctx->span_start;
+        ctx->span_start = nullptr;
+    }
+    return e;
 }
 
 // A profiled kernel slot that runs nothing: flagged, so it reads 0 ms.
@@ -369,8 +390,17 @@ int rt_reserve(rt_ctx* ctx, int32_t width, int32_t rows, int32_t num_spheres, in
     if (rc) return rc;
     rc = reserve_launch(ctx, width, rows, num_spheres, num_cubes, out_format);
     if (rc) return rc;
-    // the host API's stream (its hardware queue is set up on first use)
-    return rt_internal::ctx_stream(ctx) ? RT_OK : RT_ERR_HIP;
+    // The host API's stream, and one small pageable upload and download on
+    // it: the HIP runtime sets up its pageable-copy staging on the first
+    // such transfer of a process, which otherwise lands in the first
+    // rt_render's download (7-10 ms measured).
+    hipStream_t st = rt_internal::ctx_stream(ctx);
+    if (!st) return RT_ERR_HIP;
+    std::vector<unsigned char> tmp(std::min<size_t>(ctx->out_cap, (size_t)64 << 10));
+    HIP_TRY(hipMemcpyAsync(ctx->out_buf, tmp.data(), tmp.size(), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(tmp.data(), ctx->out_buf, tmp.size(), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return RT_OK;
 }
 
 int rt_last_kernel(rt_ctx* ctx, int32_t* kernel) {
@@ -465,12 +495,21 @@ int rt_render_path(rt_ctx* ctx, const rt_scene* scene, const float ray_dir[4],
     dscene.sphere_colours = reinterpret_cast<const float*>(sb + o_sc);
     dscene.cube_vertices = reinterpret_cast<const float*>(sb + o_cv);
     dscene.cube_colours = reinterpret_cast<const float*>(sb + o_cc);
-    HIP_TRY(hipEventRecord(ctx->ev[1], st));
+    // kernel_us: the kernels' own span (their dispatch packets' timestamps);
+    // with per-kernel profiling on, markers around them instead
+    const bool span = !ctx->profile;
+    if (span) {
+        ctx->span_start = ctx->ev[1];
+        ctx->span_stop = ctx->ev[2];
+    } else {
+        HIP_TRY(hipEventRecord(ctx->ev[1], st));
+    }
     int32_t used = 0;
     rc = render_launch(ctx, &dscene, ray_dir, d_origins, width, row_begin, row_end, out_format, path,
                 ctx->out_buf, st, &used);
+    ctx->span_start = ctx->span_stop = nullptr;
     if (rc) return rc;
-    HIP_TRY(hipEventRecord(ctx->ev[2], st));
+    if (!span) HIP_TRY(hipEventRecord(ctx->ev[2], st));
     HIP_TRY(hipMemcpyAsync(host_out, ctx->out_buf, out_bytes, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipEventRecord(ctx->ev[3], st));
     HIP_TRY(hipStreamSynchronize(st));

@@ -89,14 +89,16 @@ def main():
         order = libs if r % 2 == 0 else libs[::-1]
         for m in modes:
             for name, lib, ctx in order:
-                lib.rt_debug_set_trace_mode(ctx, m)
+                if m:  # ablations need the RT_DIAG=1 build (rt_hip_diag.h)
+                    assert lib.rt_debug_set_trace_mode(ctx, m) == 0
                 torch.cuda.synchronize()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(stream)
                 run(lib, ctx, args.steps)
                 e1.record(stream)
                 torch.cuda.synchronize()
-                lib.rt_debug_set_trace_mode(ctx, 0)
+                if m:
+                    lib.rt_debug_set_trace_mode(ctx, 0)
                 times[f"{name}" + (f"/m{m}" if m else "")].append(
                     e0.elapsed_time(e1) / args.steps * 1e3)
     res = {n: {"median_us": round(statistics.median(v), 2), "min_us": round(min(v), 2)}

@@ -7,12 +7,12 @@ R="$(cd "$(dirname "$0")/.." && pwd)"
 C="$R/opencl-ray-tracer_amd/csrc"; V="$R/opencl-ray-tracer_amd/variants"
 mkdir -p "$V"
 HIPFLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -I$R/include"
-make -s -C "$C" rt_scene.o rt_scene_device.o
+make -s -C "$C" rt_scene.o rt_scene_device.o rt_args.o
 pids=()
 for spec in "$@"; do
   name="${spec%%:*}"; flags="${spec#*:}"
   ( /opt/rocm/bin/hipcc $HIPFLAGS $flags -c -o "$V/$name.o" "$C/rt_device.hip" &&
-    /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$V/librt_hip_$name.so" "$V/$name.o" "$C/rt_scene_device.o" "$C/rt_scene.o" &&
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$V/librt_hip_$name.so" "$V/$name.o" "$C/rt_scene_device.o" "$C/rt_scene.o" "$C/rt_args.o" &&
     rm -f "$V/$name.o" && echo "built $name ($flags)" ) &
   pids+=($!)
 done
