@@ -214,8 +214,12 @@ int main(int argc, char** argv) {
         band.row_begin = row_begin + (int)((int64_t)rows * b / n_bands);
         band.row_end = row_begin + (int)((int64_t)rows * (b + 1) / n_bands);
         rc = rt_init(band.device, &band.ctx);
+        // the rest of openCLInit's one-time work, for this band's frame
+        if (rc == RT_OK)
+            rc = rt_reserve(band.ctx, width, band.row_end - band.row_begin, ns, nc, fmt);
         if (rc != RT_OK) {
-            std::fprintf(stderr, "rt_init(%d) failed: %s\n", band.device, rt_error_string(rc));
+            std::fprintf(stderr, "rt_init / rt_reserve(%d) failed: %s\n", band.device,
+                         rt_error_string(rc));
             for (Band& o : bands) rt_destroy(o.ctx);
             return 1;
         }

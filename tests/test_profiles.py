@@ -67,3 +67,23 @@ def test_traffic_matches_pmc_passes():
     assert summary["write_bytes_per_launch"] == summary["algo_bytes_per_launch"]
     assert summary["hbm_bytes_per_launch"] < 1.05 * summary["algo_bytes_per_launch"]
     assert _bench()["roofline"]["traffic"] == summary["hbm_bytes_per_launch"]
+
+
+def test_config4_traffic_matches_pmc_passes():
+    """Round 4: config 4's per-launch HBM traffic (profiles/r04/pmc_config4.json)
+    against the raw trace-kernel rows of its WRITE_SIZE / FETCH_SIZE passes:
+    the 1 GiB frame is written once (no wasted re-reads)."""
+    spec = importlib.util.spec_from_file_location("pmc_traffic",
+                                                  REPO / "scripts" / "pmc_traffic.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    r4 = REPO / "profiles" / "r04"
+    w_kb, nw = mod.per_launch(r4 / "pmc_config4_pass1.csv", "WRITE_SIZE")
+    f_kb, nf = mod.per_launch(r4 / "pmc_config4_pass2.csv", "FETCH_SIZE")
+    s = json.loads((r4 / "pmc_config4.json").read_text())
+    assert s["config"] == [8192, 8192, 192, 64, 4, "i32x4"]
+    assert s["write_bytes_per_launch"] == int(round(w_kb * 1024))
+    assert s["fetch_bytes_per_launch"] == int(round(f_kb * 1024 * 2))
+    assert s["algo_bytes_per_launch"] == 8192 * 8192 * 16
+    assert s["write_bytes_per_launch"] < 1.001 * s["algo_bytes_per_launch"]
+    assert s["hbm_bytes_per_launch"] < 1.05 * s["algo_bytes_per_launch"]
