@@ -6,7 +6,7 @@ R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$R"; mkdir -p gpurun_out; export TMPDIR=/tmp
 TAG=${TAG:-r01}
 ARGS=${BENCH_ARGS:-"--steps 10 --warmup 3 --no-cpu-baseline"}
-for mode in ${MODES:-1 2 0}; do
+for mode in ${MODES:-0}; do  # 1 2: ablations, RT_DIAG=1 library only
   timeout -k 10 200 python bench.py $ARGS --trace-mode $mode > gpurun_out/ablate_${TAG}_m$mode.json 2>gpurun_out/ablate_${TAG}_m$mode.err
   rc=$?; echo "ablation mode $mode rc=$rc"; cat gpurun_out/ablate_${TAG}_m$mode.json
   [ $rc -ne 0 ] && { tail -5 gpurun_out/ablate_${TAG}_m$mode.err; exit $rc; }
