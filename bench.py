@@ -113,6 +113,8 @@ def parse(argv=None):
                          "unmatched raises (gloo) or has its communicator aborted (RCCL, "
                          "TORCH_NCCL_ASYNC_ERROR_HANDLING=2), so the phase fails and the "
                          "later phases still run; well below --phase-deadline")
+    ap.add_argument("--init-timeout", type=float, default=600.0,
+                    help="N>1: seconds the process-group rendezvous waits for every rank")
     ap.add_argument("--phase-deadline", type=float, default=150.0,
                     help="N>1: a phase still running after this long (a hang the collective "
                          "timeout did not end) makes rank 0 print the line so far and every "
@@ -209,10 +211,12 @@ class Ctx:
         if self.distributed:
             os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
             torch.cuda.set_device(self.gpu)
-            # a stuck collective raises (gloo) or aborts (RCCL) after this
-            # long instead of blocking the run; rank 0's phase watchdog
-            # (Phases) prints the line before it
-            timeout = datetime.timedelta(seconds=args.pg_timeout)
+            # the rendezvous waits up to --init-timeout (on a fresh box the
+            # ranks' first `import torch` can take minutes and need not end
+            # together); the data-path group below, created right after,
+            # carries --pg-timeout: a stuck collective there raises (gloo) or
+            # has its communicator aborted (RCCL) after that long
+            timeout = datetime.timedelta(seconds=max(args.init_timeout, args.pg_timeout))
             if self.backend == "nccl":
                 # a collective left unmatched by a rank that failed out of a
                 # phase: after --pg-timeout the communicator is aborted and
@@ -223,8 +227,13 @@ class Ctx:
                                         timeout=timeout)
             else:
                 dist.init_process_group("gloo", timeout=timeout)
-        self.pg = None  # the data-path group: the default one until a phase fails
         self.pg_timeout = args.pg_timeout
+        # the data-path group (every measurement's collectives; replaced after
+        # a phase fails, renew_group)
+        self.pg = None
+        if self.distributed:
+            self.pg = dist.new_group(backend=self.backend,
+                                     timeout=datetime.timedelta(seconds=args.pg_timeout))
         self.dev = torch.device("cuda", self.gpu)
         # collectives move GPU tensors with RCCL, host copies with gloo
         self.coll_dev = self.dev if self.backend == "nccl" else torch.device("cpu")
