@@ -94,6 +94,7 @@ struct rt_ctx {
     hipStream_t stream = nullptr;
     // workspace (grow-only)
     void* scene_buf = nullptr;  size_t scene_cap = 0;   // host-API scene copy
+    void* scene_stage = nullptr; size_t stage_cap = 0;  // its page-locked host staging
     void* origin_buf = nullptr; size_t origin_cap = 0;  // host-API explicit origins
     void* out_buf = nullptr;    size_t out_cap = 0;     // host-API frame
     void* rec_buf = nullptr;    size_t rec_cap = 0;     // TriRec/SphRec/boxes/flag
@@ -313,8 +314,22 @@ int reserve_launch(rt_ctx* ctx, int32_t width, int32_t rows, int32_t ns, int32_t
 // rt_render's own buffers: the scene copy and the frame it downloads from.
 int reserve_host(rt_ctx* ctx, int32_t width, int32_t rows, int32_t ns, int32_t nc,
                  int32_t fmt) {
-    int rc = ensure(&ctx->scene_buf, &ctx->scene_cap, rt_args::scene_layout(ns, nc).bytes);
+    const size_t scene_bytes = rt_args::scene_layout(ns, nc).bytes;
+    int rc = ensure(&ctx->scene_buf, &ctx->scene_cap, scene_bytes);
     if (rc) return rc;
+    // the scene is packed into page-locked staging on the host and uploaded
+    // by one DMA copy, instead of five small pageable copies (grow-only)
+    if (scene_bytes > ctx->stage_cap) {
+        if (ctx->scene_stage) (void)hipHostFree(ctx->scene_stage);
+        ctx->scene_stage = nullptr;
+        ctx->stage_cap = 0;
+        const size_t n = align_up(scene_bytes + scene_bytes / 4, 1 << 16);
+        if (hipHostMalloc(&ctx->scene_stage, n, hipHostMallocDefault) != hipSuccess) {
+            ctx->scene_stage = nullptr;
+            return RT_ERR_OUT_OF_MEMORY;
+        }
+        ctx->stage_cap = n;
+    }
     return ensure(&ctx->out_buf, &ctx->out_cap, rt_args::frame_bytes(width, rows, fmt));
 }
 
@@ -413,6 +428,7 @@ void rt_destroy(rt_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->scene_stage) (void)hipHostFree(ctx->scene_stage);
     for (void* p : {ctx->scene_buf, ctx->origin_buf, ctx->out_buf, ctx->rec_buf, ctx->list_buf,
                     static_cast<void*>(ctx->flag)})
         if (p) (void)hipFree(p);
@@ -453,16 +469,24 @@ int rt_render_path(rt_ctx* ctx, const rt_scene* scene, const float ray_dir[4],
     char* sb = static_cast<char*>(ctx->scene_buf);
     hipStream_t st = rt_internal::ctx_stream(ctx);
     if (!st) return RT_ERR_HIP;
-    HIP_TRY(hipEventRecord(ctx->ev[0], st));
+    // the six uploads of MainState.cpp:759-838 as one: the arrays packed at
+    // their device offsets in page-locked staging (the previous call's copy
+    // has completed: every rt_render synchronises before it returns), then
+    // one DMA copy of the whole scene
+    char* stage = static_cast<char*>(ctx->scene_stage);
     if (ns) {
-        HIP_TRY(hipMemcpyAsync(sb + o_so, scene->sphere_origins, 16 * ns, hipMemcpyHostToDevice, st));
-        HIP_TRY(hipMemcpyAsync(sb + o_sr, scene->sphere_radius, 4 * ns, hipMemcpyHostToDevice, st));
-        HIP_TRY(hipMemcpyAsync(sb + o_sc, scene->sphere_colours, 16 * ns, hipMemcpyHostToDevice, st));
+        std::memcpy(stage + o_so, scene->sphere_origins, 16 * ns);
+        std::memcpy(stage + o_sr, scene->sphere_radius, 4 * ns);
+        std::memcpy(stage + o_sc, scene->sphere_colours, 16 * ns);
     }
     if (nc) {
-        HIP_TRY(hipMemcpyAsync(sb + o_cv, scene->cube_vertices, 16 * 36 * nc, hipMemcpyHostToDevice, st));
-        HIP_TRY(hipMemcpyAsync(sb + o_cc, scene->cube_colours, 16 * nc, hipMemcpyHostToDevice, st));
+        std::memcpy(stage + o_cv, scene->cube_vertices, 16 * 36 * nc);
+        std::memcpy(stage + o_cc, scene->cube_colours, 16 * nc);
     }
+    HIP_TRY(hipEventRecord(ctx->ev[0], st));
+    if (ns || nc)
+        HIP_TRY(hipMemcpyAsync(sb, stage, nc ? o_cc + 16 * nc : o_sc + 16 * ns,
+                               hipMemcpyHostToDevice, st));
     const float* d_origins = nullptr;
     if (ray_origins) {
         // the reference uploads all W*H origins (MainState.cpp:841-855); a
