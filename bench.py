@@ -1075,6 +1075,12 @@ def measure_host_frame(args, c: Ctx, pkg, rt, scene, w, h, fmt="i32x4"):
             step()
         ms1 = c.timed(step_one, args.steps)
         ms = c.timed(step, args.steps)
+        # the check: rank 0 poisons the frame, then one more N-rank step must
+        # rewrite every row (the one-GPU steps left a complete frame behind)
+        if c.rank == 0:
+            hf.frame.fill(0x5A5A5A5A)
+        c.dist.barrier(group=c.pg)
+        step()
         ok = c.torch.ones(1, dtype=c.torch.int32, device=c.coll_dev)
         if c.rank == 0:
             keep, ds = device_scene_from(c, scene)
