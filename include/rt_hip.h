@@ -92,8 +92,9 @@ typedef struct rt_ctx rt_ctx;
 
 /* Replaces MainState::openCLInit (MainState.cpp:1181-1326): selects HIP
  * device `device_ordinal` and loads every kernel's code object onto it (the
- * counterpart of clBuildProgram / clCreateKernel, :1302-1320), so the first
- * render pays no loading.  The stream is created on first use and the
+ * counterpart of clBuildProgram / clCreateKernel, :1302-1320) and, once per
+ * device and process, sets up the HIP runtime's staging for pageable
+ * transfers, so the first render pays no loading.  The stream is created on first use and the
  * workspace grows on demand (or up front with rt_reserve).  One context per
  * device; not re-entrant per context. */
 int rt_init(int device_ordinal, rt_ctx** out_ctx);
@@ -102,7 +103,7 @@ int rt_init(int device_ordinal, rt_ctx** out_ctx);
  * `rows` x `width` pixels with this many spheres / cubes in `out_format`:
  * the host-API scene copy and frame, the binned path's records and
  * candidate lists, and the context's stream, on which it runs one small
- * pageable upload and download (the HIP runtime's one-time staging setup).
+ * pageable upload and download (the stream's first transfers).
  * Synchronous.  openCLInit does its one-time work before any trace
  * (MainState.cpp:1290-1320, outside the trace timer :662-894); after
  * rt_reserve the first rt_render of that size allocates nothing and pays no

