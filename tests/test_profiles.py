@@ -87,3 +87,33 @@ def test_config4_traffic_matches_pmc_passes():
     assert s["algo_bytes_per_launch"] == 8192 * 8192 * 16
     assert s["write_bytes_per_launch"] < 1.001 * s["algo_bytes_per_launch"]
     assert s["hbm_bytes_per_launch"] < 1.05 * s["algo_bytes_per_launch"]
+
+
+def test_round4_bench_line_app_and_kernel_labels():
+    """Round 4's final bench line: host_path.app holds reference scenes 1-3
+    at 640x480 in both formats, every frame golden-checked, the first call's
+    kernel time within 3x of the warm median; every kernel label names a
+    kernel the library has."""
+    d = json.loads((REPO / "profiles" / "r04" / "bench_r04h.json").read_text().splitlines()[-1])
+    assert d["roofline"]["kernel"] == "trace3_kernel"
+    assert d["texture_rgba8"]["roofline"]["kernel"] == "trace3_kernel"
+    app = d["host_path"]["app"]
+    assert app["resolution"] == "640x480" and set(app["scenes"]) == {"scene1", "scene2", "scene3"}
+    for name, scene in app["scenes"].items():
+        for fmt in ("i32x4", "rgba8"):
+            e = scene[fmt]
+            assert e["frame_check"] == "bit-exact", (name, fmt)
+            assert e["kernel"] in ("frame_small_kernel", "trace3_kernel")
+            assert e["first"]["kernel_ms"] <= 3 * e["warm_median"]["kernel_ms"], (name, fmt)
+    assert app["scenes"]["scene1"]["i32x4"]["kernel"] == "frame_small_kernel"
+    assert app["scenes"]["scene3"]["i32x4"]["kernel"] == "trace3_kernel"
+
+
+def test_round4_other_configs_name_the_kernel_that_ran():
+    lines = [json.loads(l) for l in
+             (REPO / "profiles" / "r04" / "other_configs.jsonl").read_text().splitlines()]
+    by_size = {(l["config"]["width"], l["config"]["height"]): l["roofline"]["kernel"]
+               for l in lines if "config" in l}
+    assert by_size[(512, 512)] == "frame_small_kernel"      # config 1
+    assert by_size[(1920, 1080)] == "frame_small_kernel"    # config 2
+    assert by_size[(8192, 8192)] == "trace3_kernel"         # config 4
