@@ -33,6 +33,9 @@ def main():
                     help="render rank 0's band of a frame and scene scaled for this many ranks "
                          "(bench.py's weak-scaling workload)")
     ap.add_argument("--format", default="i32x4", choices=("i32x4", "rgba8"))
+    ap.add_argument("--scene", type=int, default=0,
+                    help="reference scene 1-3 at 640x480 from tests/golden instead of a "
+                         "synthetic scene")
     ap.add_argument("--kernels", action="store_true",
                     help="also per-kernel medians (rt_profile_*: HIP events on each kernel)")
     ap.add_argument("--modes", default="0",
@@ -44,8 +47,14 @@ def main():
     w, h = args.width, args.height
     k = args.k if args.k is not None else w / 640
     full_h = h * args.ranks
-    scene = pkg.Scene.synthetic(w, full_h, args.spheres * args.ranks, args.cubes * args.ranks,
-                                seed=args.seed, k=k)
+    if args.scene:
+        with np.load(REPO / "tests" / "golden" / f"scene{args.scene}_640x480.npz") as z:
+            scene = pkg.Scene(z["sphere_origins"], z["sphere_radius"], z["sphere_colours"],
+                              z["cube_vertices"], z["cube_colours"])
+        w, h, full_h = 640, 480, 480
+    else:
+        scene = pkg.Scene.synthetic(w, full_h, args.spheres * args.ranks,
+                                    args.cubes * args.ranks, seed=args.seed, k=k)
     dev = torch.device("cuda:0")
     t = {n: torch.from_numpy(np.ascontiguousarray(getattr(scene, n))).to(dev)
          for n in ("sphere_origins", "sphere_radius", "sphere_colours", "cube_vertices",
