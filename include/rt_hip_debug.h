@@ -75,8 +75,10 @@ int rt_debug_set_coarse_cull_tri(rt_ctx* ctx, int min_candidates);
 /* ... and only in frames whose primitive boxes, summed, cover the frame at
  * least `frames` times (the trace is then bound by its tests rather than its
  * stores; 0 = every frame, negative = the build's defaults: 5 for int32x4
- * renders, 0 for RGBA8 renders, whose trace is always bound by its tests).
- * A value >= 0 applies to both formats. */
+ * renders, 0 for RGBA8 renders, whose trace is bound by its tests, and in
+ * either format only in bands of at least 768 coarse bins, since fewer coarse
+ * waves cannot hide the cull's latency).  A value >= 0 applies to both
+ * formats and every band size. */
 int rt_debug_set_coarse_cull_overdraw(rt_ctx* ctx, int frames);
 /* The bounds tri_t_bounds gives the trace's computed fp64 t over pixels
  * [xa, xb] x [ya, yb] (host evaluation; returns 0 without a bound). */

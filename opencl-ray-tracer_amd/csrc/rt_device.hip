@@ -86,6 +86,14 @@
                                          // frame (its trace is bound by its tests, not by
                                          // its stores)
 #endif
+#ifndef RT_COARSE_CULL_TRI_BINS
+#define RT_COARSE_CULL_TRI_BINS 768  // triangles join the cull only in bands of at least this
+                                     // many coarse bins: fewer coarse waves run as one
+                                     // generation and cannot hide the cull's latency (round 4:
+                                     // 640x480 to 1920x1080 frames 1-27 us slower with it at
+                                     // box overdraw 5-20, 2560x1440 up to 16 us faster;
+                                     // DESIGN.md §3.5)
+#endif
 
 // ===========================================================================
 // Host side
@@ -126,6 +134,8 @@ struct rt_ctx {
     // (int32x4 renders; RGBA8 renders take the second gate)
     unsigned coarse_cull_overdraw = RT_COARSE_CULL_OVERDRAW;
     unsigned coarse_cull_overdraw_rgba8 = RT_COARSE_CULL_OVERDRAW_RGBA8;
+    // ... in bands of at least this many coarse bins
+    int64_t coarse_cull_tri_bins = RT_COARSE_CULL_TRI_BINS;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     // rt_render's kernel span: ev[1] / ev[2] ride on the first / last kernel
     // of the render (set only while rt_render_path enqueues it)
@@ -841,6 +851,9 @@ int rt_debug_set_coarse_cull_overdraw(rt_ctx* ctx, int frames) {
     ctx->coarse_cull_overdraw = frames < 0 ? RT_COARSE_CULL_OVERDRAW : (unsigned)frames;
     ctx->coarse_cull_overdraw_rgba8 =
         frames < 0 ? RT_COARSE_CULL_OVERDRAW_RGBA8 : (unsigned)frames;
+    // an explicit gate applies to every band size (the tests force the cull
+    // on small frames this way)
+    ctx->coarse_cull_tri_bins = frames < 0 ? RT_COARSE_CULL_TRI_BINS : 0;
     return RT_OK;
 }
 

@@ -68,14 +68,23 @@ def main():
     fmt = 0 if args.format == "i32x4" else 1
     out = torch.empty((h, w, 4) if fmt == 0 else (h, w), dtype=torch.int32, device=dev)
     libs = []
-    for path in args.libs:
+    for spec in args.libs:
+        # "path@setter=value,...": the same library with rt_debug_set_<setter>
+        # applied (e.g. @coarse_cull_tri=0), timed as a variant of its own
+        path, _, sets = spec.partition("@")
         lib = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
         ctx = ctypes.c_void_p()
         assert lib.rt_init(0, ctypes.byref(ctx)) == 0
+        for kv in filter(None, sets.split(",")):
+            k, v = kv.split("=")
+            fn = getattr(lib, f"rt_debug_set_{k}")
+            fn.argtypes = [ctypes.c_void_p, ctypes.c_int64 if k == "list_budget" else ctypes.c_int]
+            assert fn(ctx, int(v)) == 0, kv
         lib.rt_render_device.argtypes = [ctypes.c_void_p, ctypes.POINTER(pkg._Scene),
                                          ctypes.c_void_p, ctypes.c_void_p] + \
             [ctypes.c_int32] * 6 + [ctypes.c_void_p, ctypes.c_void_p]
-        libs.append((Path(path).stem.replace("librt_hip_", ""), lib, ctx))
+        libs.append((Path(path).stem.replace("librt_hip_", "") + (f"@{sets}" if sets else ""),
+                     lib, ctx))
 
     def run(lib, ctx, n):
         for _ in range(n):
