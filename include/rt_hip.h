@@ -57,7 +57,9 @@ enum {
     RT_KERNEL_TRACE = 1,        /* prep_kernel -> coarse3_kernel -> trace3_kernel */
     RT_KERNEL_TRACE_SMALL = 2,  /* prep_kernel -> trace_small_kernel (<= 512 primitives) */
     RT_KERNEL_FRAME_SMALL = 3,  /* frame_small_kernel, one launch (<= 128 primitives) */
-    RT_KERNEL_GENERIC = 4       /* generic_kernel: explicit origins / any direction */
+    RT_KERNEL_GENERIC = 4,      /* generic_kernel: explicit origins / any direction */
+    RT_KERNEL_TRACE_SPLIT = 5   /* prep_kernel -> coarse3_kernel -> trace3_split_kernel
+                                   (small frames: several waves per wave tile) */
 };
 
 typedef struct rt_scene {

@@ -63,6 +63,12 @@ int rt_debug_set_small_path(rt_ctx* ctx, int enable);
  * grid is resident at once, 2 = on every frame size (tests), 0 = prep_kernel
  * + trace_small_kernel (A/B and tests).  Needs the small path (above). */
 int rt_debug_set_small_fused(rt_ctx* ctx, int enable);
+
+/* Waves per wave tile in the binned trace: 0 (default) = by frame size
+ * (trace3_split_kernel, 4 / 2 waves per tile, on frames of at most 2048 /
+ * 4096 wave tiles), 1 = always one (trace3_kernel), 2 or 4 = always that
+ * many. */
+int rt_debug_set_trace_split(rt_ctx* ctx, int waves);
 /* Coarse depth cull of sphere candidates in coarse bins with at least
  * `enable` sphere candidates (1 = every bin, 0 = off: every candidate the tile
  * classifier keeps stays; negative = the build's default; A/B and tests). */

@@ -49,7 +49,7 @@ EXPORTED_SYMBOLS = (
 )
 # rt_last_kernel's codes (RT_KERNEL_*, rt_hip.h) by name
 KERNEL_NAMES = {0: None, 1: "trace3_kernel", 2: "trace_small_kernel", 3: "frame_small_kernel",
-                4: "generic_kernel"}
+                4: "generic_kernel", 5: "trace3_split_kernel"}
 # exported only by the diagnostics build (make RT_DIAG=1, include/rt_hip_diag.h)
 DIAG_SYMBOLS = ("rt_debug_set_trace_mode",)
 
@@ -163,6 +163,7 @@ def library() -> ctypes.CDLL:
         "rt_debug_set_coarse_cull_tri": (ctypes.c_int, [vp, ctypes.c_int]),
         "rt_debug_set_coarse_cull_overdraw": (ctypes.c_int, [vp, ctypes.c_int]),
         "rt_debug_set_small_fused": (ctypes.c_int, [vp, ctypes.c_int]),
+        "rt_debug_set_trace_split": (ctypes.c_int, [vp, ctypes.c_int]),
         "rt_debug_triangle_t_bounds": (ctypes.c_int, [vp, vp, vp, vp, i32, i32, i32, i32, i32,
                                                       i32, i32, vp]),
         "rt_debug_triangle_box_wide": (ctypes.c_int, [vp, vp, vp, vp, i32, i32, i32, vp, vp]),
@@ -548,6 +549,13 @@ class RayTracer:
         (2), or prep + trace_small_kernel (0) (diagnostics / tests)."""
         _check(library().rt_debug_set_small_fused(self._ctx, int(mode)),
                "rt_debug_set_small_fused")
+
+    def set_trace_split(self, waves: int) -> None:
+        """Waves per wave tile in the binned trace: 0 = by frame size
+        (trace3_split_kernel on small frames, default), 1 = trace3_kernel,
+        2 / 4 = trace3_split_kernel with that many (diagnostics / tests)."""
+        _check(library().rt_debug_set_trace_split(self._ctx, int(waves)),
+               "rt_debug_set_trace_split")
 
     def set_coarse_cull_tri(self, min_candidates: int) -> None:
         """Diagnostics: triangles join the coarse depth cull in bins with at

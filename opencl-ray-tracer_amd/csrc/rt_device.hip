@@ -86,6 +86,14 @@
                                          // frame (its trace is bound by its tests, not by
                                          // its stores)
 #endif
+#ifndef RT_SPLIT4_TILES
+#define RT_SPLIT4_TILES 2048  // trace3_split_kernel with 4 waves per tile up to this many tiles
+#endif
+#ifndef RT_SPLIT2_TILES
+#define RT_SPLIT2_TILES 4096  // ... with 2 waves per tile up to this many (round 4: at
+                              // 8160, 1920x1080, flat; 4 waves win below 2048 tiles,
+                              // 2 up to 4096, one above)
+#endif
 #ifndef RT_COARSE_CULL_TRI_BINS
 #define RT_COARSE_CULL_TRI_BINS 768  // triangles join the cull only in bands of at least this
                                      // many coarse bins: fewer coarse waves run as one
@@ -122,6 +130,9 @@ struct rt_ctx {
     // <= 64 x RT_FUSED_CHUNKS primitives on frames whose grid is resident at
     // once: frame_small_kernel (1; 2 = on every frame size, tests; 0 = off)
     int small_fused = RT_SMALL_FUSED;
+    // waves per wave tile in the binned trace: 0 = by frame size
+    // (trace3_split_kernel on small frames), 1 = one (trace3_kernel), 2 / 4
+    int trace_split = 0;
     int n_cu = 256;  // compute units (rt_init)
     // coarse depth cull of sphere candidates in bins with at least this many
     // candidates (0 = off)
@@ -878,6 +889,12 @@ int rt_debug_triangle_t_bounds(const float v0[3], const float v1[3], const float
 int rt_debug_set_small_fused(rt_ctx* ctx, int enable) {
     if (!ctx || enable < 0 || enable > 2) return RT_ERR_INVALID_ARG;
     ctx->small_fused = enable;
+    return RT_OK;
+}
+
+int rt_debug_set_trace_split(rt_ctx* ctx, int waves) {
+    if (!ctx || !(waves == 0 || waves == 1 || waves == 2 || waves == 4)) return RT_ERR_INVALID_ARG;
+    ctx->trace_split = waves;
     return RT_OK;
 }
 

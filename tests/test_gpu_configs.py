@@ -311,6 +311,46 @@ def test_coarse_depth_cull_exact(pkg, rt, oracle, case):
     assert np.array_equal(on, want)
 
 
+@pytest.mark.parametrize("case", ["ties", "cube_ties", "dense_cubes", "dense_rgba8",
+                                  "band", "wide"])
+def test_trace_split_exact(pkg, rt, oracle, case):
+    """trace3_split_kernel (2 or 4 waves per wave tile, each testing every
+    2nd / 4th candidate the tile keeps, merged by smallest t then smallest
+    slot) gives trace3_kernel's frame and the oracle's, with exact ties of
+    spheres and of cubes (the first in primitive order must win,
+    MainState.cpp:386-391), in both formats, on a row band and in the wide
+    tile build."""
+    fmt = "rgba8" if case.endswith("rgba8") else "i32x4"
+    w, h, rows = 640, 480, (0, 480)
+    if case == "ties":
+        scene = _tie_scene(pkg, w, h, 400, 4)
+    elif case == "cube_ties":
+        scene = _cube_tie_scene(pkg, w, h, 13)
+    elif case == "band":
+        scene, rows = _cube_tie_scene(pkg, w, h, 14), (77, 401)
+    else:
+        scene = pkg.Scene.synthetic(w, h, 120, 200, seed=11, k=w / 640 * 3)
+    frames = {}
+    try:
+        rt.set_small_path(False)  # (every case takes the binned trace)
+        if case == "wide":
+            rt.set_tile_variant(2)
+        for split in (1, 2, 4):
+            rt.set_trace_split(split)
+            frames[split], t = rt.render(scene, w, h, rows=rows, fmt=fmt)
+            assert t.path == "binned"
+            assert rt.last_kernel() == ("trace3_kernel" if split == 1 else "trace3_split_kernel")
+    finally:
+        rt.set_trace_split(0)
+        rt.set_tile_variant(0)
+        rt.set_small_path(True)
+    want = oracle.trace(scene, w, h, rows=rows, threads=THREADS)
+    if fmt == "rgba8":
+        want = oracle.pack_rgba8(want)
+    for split, got in frames.items():
+        assert np.array_equal(got, want), split
+
+
 def test_render_into_registered_host_frame(pkg, rt):
     """rt_host_register: rt_render's download into a page-locked host frame
     (the app's `pixels` vector) gives the same frame, for bands too."""
@@ -371,8 +411,9 @@ def test_randomized_parity_sweep(pkg, rt, oracle, seed):
     """Seeded random frames against the oracle: frame sizes from 96 to 1500
     px a side, 1 to 600 spheres and 0 to 80 cubes at random densities, row
     bands, both formats, both tile builds, the depth culls forced on or left
-    at their gates, the one-kernel small-scene path on / off / forced, and bin
-    masks or box scans.  Each
+    at their gates, the one-kernel small-scene path on / off / forced, bin
+    masks or box scans, and 1 / 2 / 4 waves per wave tile in the trace (or
+    the frame-size choice).  Each
     knob is drawn independently from the seed's generator, so no two are
     tied to each other across the sweep."""
     rng = np.random.default_rng(1000 + seed)
@@ -391,8 +432,11 @@ def test_randomized_parity_sweep(pkg, rt, oracle, seed):
     small_fused = int(rng.integers(0, 3))
     cull_all = bool(rng.integers(0, 2))
     bin_masks = bool(rng.random() < 0.75)
-    knobs = dict(tile=tile, small_fused=small_fused, cull_all=cull_all, bin_masks=bin_masks)
+    split = int(rng.choice([0, 1, 2, 4]))  # waves per wave tile in the binned trace
+    knobs = dict(tile=tile, small_fused=small_fused, cull_all=cull_all, bin_masks=bin_masks,
+                 split=split)
     try:
+        rt.set_trace_split(split)
         rt.set_tile_variant(tile)
         rt.set_small_fused(small_fused)
         rt.set_bin_masks(bin_masks)
@@ -402,6 +446,7 @@ def test_randomized_parity_sweep(pkg, rt, oracle, seed):
             rt.set_coarse_cull_overdraw(0)
         got, t = rt.render(scene, w, h, rows=rows, fmt=fmt)
     finally:
+        rt.set_trace_split(0)
         rt.set_tile_variant(0)
         rt.set_small_fused(1)
         rt.set_bin_masks(True)

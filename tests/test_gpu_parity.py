@@ -810,13 +810,16 @@ def test_fresh_context_first_render(pkg):
 def test_last_kernel_names_the_path_taken(pkg, rt, oracle):
     """rt_last_kernel reports the kernel that actually ran (the bench's
     `kernel` label): frame_small_kernel for <= 128 primitives on a resident
-    grid, trace_small_kernel for <= 512, trace3_kernel beyond, generic_kernel
-    for the brute-force path."""
+    grid, trace_small_kernel for <= 512, trace3_kernel beyond (on frames of
+    at most 4096 wave tiles trace3_split_kernel), generic_kernel for the
+    brute-force path."""
     cases = [(pkg.Scene.synthetic(1920, 1080, 16, 4, seed=2, k=3.0), 1920, 1080, "auto",
               "frame_small_kernel"),
              (pkg.Scene.synthetic(4096, 1024, 100, 30, seed=5, k=6.4), 4096, 1024, "auto",
               "trace_small_kernel"),
              (pkg.Scene.synthetic(1024, 1024, 256, 64, seed=3, k=1.6), 1024, 1024, "auto",
+              "trace3_split_kernel"),
+             (pkg.Scene.synthetic(2048, 2048, 256, 64, seed=3, k=3.2), 2048, 2048, "auto",
               "trace3_kernel"),
              (pkg.Scene.synthetic(256, 128, 8, 2, seed=1, k=0.4), 256, 128, "generic",
               "generic_kernel")]
