@@ -69,6 +69,10 @@ int rt_debug_set_small_fused(rt_ctx* ctx, int enable);
  * 4096 wave tiles), 1 = always one (trace3_kernel), 2 or 4 = always that
  * many. */
 int rt_debug_set_trace_split(rt_ctx* ctx, int waves);
+
+/* Waves per coarse bin (coarse3_kernel): 0 (default) = by band size (4 up to
+ * 1024 bins, then 1), or always 1, 2 or 4. */
+int rt_debug_set_coarse_waves(rt_ctx* ctx, int waves);
 /* Coarse depth cull of sphere candidates in coarse bins with at least
  * `enable` sphere candidates (1 = every bin, 0 = off: every candidate the tile
  * classifier keeps stays; negative = the build's default; A/B and tests). */

@@ -164,6 +164,7 @@ def library() -> ctypes.CDLL:
         "rt_debug_set_coarse_cull_overdraw": (ctypes.c_int, [vp, ctypes.c_int]),
         "rt_debug_set_small_fused": (ctypes.c_int, [vp, ctypes.c_int]),
         "rt_debug_set_trace_split": (ctypes.c_int, [vp, ctypes.c_int]),
+        "rt_debug_set_coarse_waves": (ctypes.c_int, [vp, ctypes.c_int]),
         "rt_debug_triangle_t_bounds": (ctypes.c_int, [vp, vp, vp, vp, i32, i32, i32, i32, i32,
                                                       i32, i32, vp]),
         "rt_debug_triangle_box_wide": (ctypes.c_int, [vp, vp, vp, vp, i32, i32, i32, vp, vp]),
@@ -556,6 +557,12 @@ class RayTracer:
         2 / 4 = trace3_split_kernel with that many (diagnostics / tests)."""
         _check(library().rt_debug_set_trace_split(self._ctx, int(waves)),
                "rt_debug_set_trace_split")
+
+    def set_coarse_waves(self, waves: int) -> None:
+        """Waves per coarse bin: 0 = by band size (default), 1 / 2 / 4
+        (diagnostics / tests)."""
+        _check(library().rt_debug_set_coarse_waves(self._ctx, int(waves)),
+               "rt_debug_set_coarse_waves")
 
     def set_coarse_cull_tri(self, min_candidates: int) -> None:
         """Diagnostics: triangles join the coarse depth cull in bins with at

@@ -94,6 +94,14 @@
                               // 8160, 1920x1080, flat; 4 waves win below 2048 tiles,
                               // 2 up to 4096, one above)
 #endif
+#ifndef RT_COARSE_W4_BINS
+#define RT_COARSE_W4_BINS 1024  // coarse3_kernel with 4 waves per bin in bands up to this many
+                                // bins (round 4: 4 waves fastest from 80 to 920 bins, one
+                                // at 4096 and up)
+#endif
+#ifndef RT_COARSE_W2_BINS
+#define RT_COARSE_W2_BINS 1024  // ... with 2 waves per bin up to this many (none by default)
+#endif
 #ifndef RT_COARSE_CULL_TRI_BINS
 #define RT_COARSE_CULL_TRI_BINS 768  // triangles join the cull only in bands of at least this
                                      // many coarse bins: fewer coarse waves run as one
@@ -133,6 +141,8 @@ struct rt_ctx {
     // waves per wave tile in the binned trace: 0 = by frame size
     // (trace3_split_kernel on small frames), 1 = one (trace3_kernel), 2 / 4
     int trace_split = 0;
+    // waves per coarse bin: 0 = by band size, 1 / 2 / 4
+    int coarse_waves = 0;
     int n_cu = 256;  // compute units (rt_init)
     // coarse depth cull of sphere candidates in bins with at least this many
     // candidates (0 = off)
@@ -895,6 +905,12 @@ int rt_debug_set_small_fused(rt_ctx* ctx, int enable) {
 int rt_debug_set_trace_split(rt_ctx* ctx, int waves) {
     if (!ctx || !(waves == 0 || waves == 1 || waves == 2 || waves == 4)) return RT_ERR_INVALID_ARG;
     ctx->trace_split = waves;
+    return RT_OK;
+}
+
+int rt_debug_set_coarse_waves(rt_ctx* ctx, int waves) {
+    if (!ctx || !(waves == 0 || waves == 1 || waves == 2 || waves == 4)) return RT_ERR_INVALID_ARG;
+    ctx->coarse_waves = waves;
     return RT_OK;
 }
 

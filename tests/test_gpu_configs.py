@@ -351,6 +351,54 @@ def test_trace_split_exact(pkg, rt, oracle, case):
         assert np.array_equal(got, want), split
 
 
+@pytest.mark.parametrize("case", ["ties", "cube_ties", "dense_culled", "dense_rgba8",
+                                  "band", "box_scan", "wide"])
+def test_coarse_waves_exact(pkg, rt, oracle, case):
+    """coarse3_kernel with 1 / 2 / 4 waves per bin (the waves share the
+    staging loads and the (candidate, tile) pair loops; wave 0 writes the
+    list) gives the same frame, equal to the oracle: sphere and cube ties,
+    the depth culls forced on in every bin (spheres and triangles), RGBA8, a
+    row band, the box-scan path and the wide tile build."""
+    fmt = "rgba8" if case.endswith("rgba8") else "i32x4"
+    w, h, rows = 640, 480, (0, 480)
+    if case == "ties":
+        scene = _tie_scene(pkg, w, h, 400, 5)
+    elif case == "cube_ties":
+        scene = _cube_tie_scene(pkg, w, h, 15)
+    elif case == "band":
+        scene, rows = _cube_tie_scene(pkg, w, h, 16), (33, 350)
+    else:
+        scene = pkg.Scene.synthetic(w, h, 300, 120, seed=12, k=w / 640 * 4)
+    frames = {}
+    try:
+        rt.set_small_path(False)
+        if case in ("dense_culled", "dense_rgba8", "ties", "cube_ties"):
+            rt.set_coarse_cull(1)  # every bin, spheres and triangles
+            rt.set_coarse_cull_tri(1)
+            rt.set_coarse_cull_overdraw(0)
+        if case == "box_scan":
+            rt.set_bin_masks(False)
+        if case == "wide":
+            rt.set_tile_variant(2)
+        for cw in (1, 2, 4):
+            rt.set_coarse_waves(cw)
+            frames[cw], t = rt.render(scene, w, h, rows=rows, fmt=fmt)
+            assert t.path == "binned"
+    finally:
+        rt.set_coarse_waves(0)
+        rt.set_coarse_cull(-1)
+        rt.set_coarse_cull_tri(-1)
+        rt.set_coarse_cull_overdraw(-1)
+        rt.set_bin_masks(True)
+        rt.set_tile_variant(0)
+        rt.set_small_path(True)
+    want = oracle.trace(scene, w, h, rows=rows, threads=THREADS)
+    if fmt == "rgba8":
+        want = oracle.pack_rgba8(want)
+    for cw, got in frames.items():
+        assert np.array_equal(got, want), cw
+
+
 def test_render_into_registered_host_frame(pkg, rt):
     """rt_host_register: rt_render's download into a page-locked host frame
     (the app's `pixels` vector) gives the same frame, for bands too."""
@@ -412,8 +460,8 @@ def test_randomized_parity_sweep(pkg, rt, oracle, seed):
     px a side, 1 to 600 spheres and 0 to 80 cubes at random densities, row
     bands, both formats, both tile builds, the depth culls forced on or left
     at their gates, the one-kernel small-scene path on / off / forced, bin
-    masks or box scans, and 1 / 2 / 4 waves per wave tile in the trace (or
-    the frame-size choice).  Each
+    masks or box scans, and 1 / 2 / 4 waves per wave tile in the trace and
+    per coarse bin (or the frame-size choices).  Each
     knob is drawn independently from the seed's generator, so no two are
     tied to each other across the sweep."""
     rng = np.random.default_rng(1000 + seed)
@@ -433,10 +481,12 @@ def test_randomized_parity_sweep(pkg, rt, oracle, seed):
     cull_all = bool(rng.integers(0, 2))
     bin_masks = bool(rng.random() < 0.75)
     split = int(rng.choice([0, 1, 2, 4]))  # waves per wave tile in the binned trace
+    coarse_waves = int(rng.choice([0, 1, 2, 4]))  # waves per coarse bin
     knobs = dict(tile=tile, small_fused=small_fused, cull_all=cull_all, bin_masks=bin_masks,
-                 split=split)
+                 split=split, coarse_waves=coarse_waves)
     try:
         rt.set_trace_split(split)
+        rt.set_coarse_waves(coarse_waves)
         rt.set_tile_variant(tile)
         rt.set_small_fused(small_fused)
         rt.set_bin_masks(bin_masks)
@@ -447,6 +497,7 @@ def test_randomized_parity_sweep(pkg, rt, oracle, seed):
         got, t = rt.render(scene, w, h, rows=rows, fmt=fmt)
     finally:
         rt.set_trace_split(0)
+        rt.set_coarse_waves(0)
         rt.set_tile_variant(0)
         rt.set_small_fused(1)
         rt.set_bin_masks(True)
