@@ -70,8 +70,8 @@ int rt_debug_set_small_fused(rt_ctx* ctx, int enable);
  * many. */
 int rt_debug_set_trace_split(rt_ctx* ctx, int waves);
 
-/* Waves per coarse bin (coarse3_kernel): 0 (default) = by band size (4 up to
- * 1024 bins, then 1), or always 1, 2 or 4. */
+/* Waves per coarse bin (coarse3_kernel): 0 (default) = by band size (8 up to
+ * 256 bins, 4 up to 1024, then 1), or always 1, 2, 4 or 8. */
 int rt_debug_set_coarse_waves(rt_ctx* ctx, int waves);
 /* Coarse depth cull of sphere candidates in coarse bins with at least
  * `enable` sphere candidates (1 = every bin, 0 = off: every candidate the tile

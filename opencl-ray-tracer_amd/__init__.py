@@ -559,7 +559,7 @@ class RayTracer:
                "rt_debug_set_trace_split")
 
     def set_coarse_waves(self, waves: int) -> None:
-        """Waves per coarse bin: 0 = by band size (default), 1 / 2 / 4
+        """Waves per coarse bin: 0 = by band size (default), 1 / 2 / 4 / 8
         (diagnostics / tests)."""
         _check(library().rt_debug_set_coarse_waves(self._ctx, int(waves)),
                "rt_debug_set_coarse_waves")

@@ -330,6 +330,8 @@ def test_trace_split_exact(pkg, rt, oracle, case):
         scene, rows = _cube_tie_scene(pkg, w, h, 14), (77, 401)
     else:
         scene = pkg.Scene.synthetic(w, h, 120, 200, seed=11, k=w / 640 * 3)
+    with pytest.raises(pkg.RtError):
+        rt.set_trace_split(8)  # (at most 4 waves per tile: the merge's LDS)
     frames = {}
     try:
         rt.set_small_path(False)  # (every case takes the binned trace)
@@ -380,7 +382,7 @@ def test_coarse_waves_exact(pkg, rt, oracle, case):
             rt.set_bin_masks(False)
         if case == "wide":
             rt.set_tile_variant(2)
-        for cw in (1, 2, 4):
+        for cw in (1, 2, 4, 8):
             rt.set_coarse_waves(cw)
             frames[cw], t = rt.render(scene, w, h, rows=rows, fmt=fmt)
             assert t.path == "binned"
@@ -481,7 +483,7 @@ def test_randomized_parity_sweep(pkg, rt, oracle, seed):
     cull_all = bool(rng.integers(0, 2))
     bin_masks = bool(rng.random() < 0.75)
     split = int(rng.choice([0, 1, 2, 4]))  # waves per wave tile in the binned trace
-    coarse_waves = int(rng.choice([0, 1, 2, 4]))  # waves per coarse bin
+    coarse_waves = int(rng.choice([0, 1, 2, 4, 8]))  # waves per coarse bin
     knobs = dict(tile=tile, small_fused=small_fused, cull_all=cull_all, bin_masks=bin_masks,
                  split=split, coarse_waves=coarse_waves)
     try:
