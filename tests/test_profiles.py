@@ -89,6 +89,26 @@ def test_config4_traffic_matches_pmc_passes():
     assert s["hbm_bytes_per_launch"] < 1.05 * s["algo_bytes_per_launch"]
 
 
+def test_config3_final_traffic_matches_pmc_passes():
+    """Round 4's final library (raw buffer frame stores): config 3's traffic
+    file, which bench.py's `roofline.traffic` reads by default
+    (profiles/r04_pmc_config3.json), against the raw trace-kernel rows of its
+    WRITE_SIZE / FETCH_SIZE passes: the frame is written exactly once."""
+    spec = importlib.util.spec_from_file_location("pmc_traffic",
+                                                  REPO / "scripts" / "pmc_traffic.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    r4 = REPO / "profiles" / "r04"
+    w_kb, _ = mod.per_launch(r4 / "pmc_config3_final_pass1.csv", "WRITE_SIZE")
+    f_kb, _ = mod.per_launch(r4 / "pmc_config3_final_pass2.csv", "FETCH_SIZE")
+    s = json.loads((REPO / "profiles" / "r04_pmc_config3.json").read_text())
+    assert s["config"] == [4096, 4096, 256, 64, 3, "i32x4"]
+    assert s["write_bytes_per_launch"] == int(round(w_kb * 1024))
+    assert s["fetch_bytes_per_launch"] == int(round(f_kb * 1024 * 2))
+    assert s["write_bytes_per_launch"] == s["algo_bytes_per_launch"] == 4096 * 4096 * 16
+    assert s["hbm_bytes_per_launch"] < 1.05 * s["algo_bytes_per_launch"]
+
+
 def test_round4_bench_line_app_and_kernel_labels():
     """Round 4's final bench line: host_path.app holds reference scenes 1-3
     at 640x480 in both formats, every frame golden-checked, the first call's
