@@ -58,8 +58,9 @@ enum {
     RT_KERNEL_TRACE_SMALL = 2,  /* prep_kernel -> trace_small_kernel (<= 512 primitives) */
     RT_KERNEL_FRAME_SMALL = 3,  /* frame_small_kernel, one launch (<= 128 primitives) */
     RT_KERNEL_GENERIC = 4,      /* generic_kernel: explicit origins / any direction */
-    RT_KERNEL_TRACE_SPLIT = 5   /* prep_kernel -> coarse3_kernel -> trace3_split_kernel
+    RT_KERNEL_TRACE_SPLIT = 5,  /* prep_kernel -> coarse3_kernel -> trace3_split_kernel
                                    (small frames: several waves per wave tile) */
+    RT_KERNEL_TRACE_BIN = 6     /* prep_kernel -> trace_bin_kernel (tiles bin themselves) */
 };
 
 typedef struct rt_scene {

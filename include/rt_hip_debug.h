@@ -73,6 +73,13 @@ int rt_debug_set_trace_split(rt_ctx* ctx, int waves);
 /* Waves per coarse bin (coarse3_kernel): 0 (default) = by band size (8 up to
  * 256 bins, 4 up to 1024, then 1), or always 1, 2, 4 or 8. */
 int rt_debug_set_coarse_waves(rt_ctx* ctx, int waves);
+
+/* Binned frames without the coarse kernel (trace_bin_kernel: every wave tile
+ * ANDs its bin's mask words and classifies the candidates itself; scenes of
+ * at most 1024 primitives): 0 (default) = automatic (int32x4 frames above
+ * 4096 wave tiles whose previous binned frame on this context had a box
+ * overdraw below 6 frames), 1 = wherever it applies, 2 = never. */
+int rt_debug_set_trace_bin(rt_ctx* ctx, int mode);
 /* Coarse depth cull of sphere candidates in coarse bins with at least
  * `enable` sphere candidates (1 = every bin, 0 = off: every candidate the tile
  * classifier keeps stays; negative = the build's default; A/B and tests). */

@@ -49,7 +49,7 @@ EXPORTED_SYMBOLS = (
 )
 # rt_last_kernel's codes (RT_KERNEL_*, rt_hip.h) by name
 KERNEL_NAMES = {0: None, 1: "trace3_kernel", 2: "trace_small_kernel", 3: "frame_small_kernel",
-                4: "generic_kernel", 5: "trace3_split_kernel"}
+                4: "generic_kernel", 5: "trace3_split_kernel", 6: "trace_bin_kernel"}
 # exported only by the diagnostics build (make RT_DIAG=1, include/rt_hip_diag.h)
 DIAG_SYMBOLS = ("rt_debug_set_trace_mode",)
 
@@ -165,6 +165,7 @@ def library() -> ctypes.CDLL:
         "rt_debug_set_small_fused": (ctypes.c_int, [vp, ctypes.c_int]),
         "rt_debug_set_trace_split": (ctypes.c_int, [vp, ctypes.c_int]),
         "rt_debug_set_coarse_waves": (ctypes.c_int, [vp, ctypes.c_int]),
+        "rt_debug_set_trace_bin": (ctypes.c_int, [vp, ctypes.c_int]),
         "rt_debug_triangle_t_bounds": (ctypes.c_int, [vp, vp, vp, vp, i32, i32, i32, i32, i32,
                                                       i32, i32, vp]),
         "rt_debug_triangle_box_wide": (ctypes.c_int, [vp, vp, vp, vp, i32, i32, i32, vp, vp]),
@@ -563,6 +564,13 @@ class RayTracer:
         (diagnostics / tests)."""
         _check(library().rt_debug_set_coarse_waves(self._ctx, int(waves)),
                "rt_debug_set_coarse_waves")
+
+    def set_trace_bin(self, mode: int) -> None:
+        """Binned frames without the coarse kernel (trace_bin_kernel: every
+        wave tile classifies its bin's candidates itself): 0 = automatic
+        (default), 1 = wherever it applies, 2 = never (diagnostics / tests)."""
+        _check(library().rt_debug_set_trace_bin(self._ctx, int(mode)),
+               "rt_debug_set_trace_bin")
 
     def set_coarse_cull_tri(self, min_candidates: int) -> None:
         """Diagnostics: triangles join the coarse depth cull in bins with at

@@ -106,6 +106,12 @@
 #ifndef RT_COARSE_W2_BINS
 #define RT_COARSE_W2_BINS 1024  // ... with 2 waves per bin up to this many (none by default)
 #endif
+#ifndef RT_TRACE_BIN_OD
+#define RT_TRACE_BIN_OD 6  // trace_bin_kernel (auto) below this box overdraw, in frames (round 4:
+                           // config 3 (2.8) and 4096x4096 / 2560x1440 / 3840x2160 scenes of
+                           // overdraw 3-5 faster without the coarse kernel, overdraw 11+
+                           // 1.5-4x slower without its depth culls)
+#endif
 #ifndef RT_COARSE_CULL_TRI_BINS
 #define RT_COARSE_CULL_TRI_BINS 768  // triangles join the cull only in bands of at least this
                                      // many coarse bins: fewer coarse waves run as one
@@ -129,6 +135,15 @@ struct rt_ctx {
     void* rec_buf = nullptr;    size_t rec_cap = 0;     // TriRec/SphRec/boxes/flag
     void* list_buf = nullptr;   size_t list_cap = 0;    // coarse-bin candidate lists
     unsigned* flag = nullptr;   // non-finite scene flag (generation-stamped)
+    // a recent binned frame's overdraw verdict (0 = none yet, 1 = below
+    // RT_TRACE_BIN_OD frames, 2 = not): the coarse or self-binning trace
+    // kernel writes it to flag word 6 (device memory), and every 8th binned
+    // launch copies it asynchronously into this page-locked word, which picks
+    // the next int32x4 frame's path (performance only; both paths are exact)
+    // Its lifetime is the context's: allocated in rt_init, freed only in
+    // rt_destroy after every copy into it has landed.
+    unsigned* od_verdict = nullptr;
+    unsigned verdict_copies = 0;  // copies enqueued (rt_destroy syncs the device if any)
     unsigned gen = 0;
     unsigned od_launches = 0;  // binned launches: picks the box-overdraw slot
     int trace_mode = 0;  // diagnostics ablation (RT_DIAG builds), see trace3_kernel
@@ -145,8 +160,12 @@ struct rt_ctx {
     // waves per wave tile in the binned trace: 0 = by frame size
     // (trace3_split_kernel on small frames), 1 = one (trace3_kernel), 2 / 4
     int trace_split = 0;
-    // waves per coarse bin: 0 = by band size, 1 / 2 / 4
+    // waves per coarse bin: 0 = by band size, 1 / 2 / 4 / 8
     int coarse_waves = 0;
+    // binned frames without the coarse kernel (trace_bin_kernel): 0 = auto
+    // (int32x4 frames above the split sizes whose last binned frame had a box
+    // overdraw below RT_TRACE_BIN_OD), 1 = always where it applies, 2 = never
+    int trace_bin = 0;
     int n_cu = 256;  // compute units (rt_init)
     // coarse depth cull of sphere candidates in bins with at least this many
     // candidates (0 = off)
@@ -437,12 +456,19 @@ int rt_init(int device_ordinal, rt_ctx** out_ctx) {
         }
     }
     // [0] non-finite flag, [1] explicit-origin grid check, [2..5] two
-    // 64-bit box-overdraw slots (see launch())
+    // 64-bit box-overdraw slots, [6] the overdraw verdict (see launch())
     if (hipMalloc(&ctx->flag, 8 * sizeof(unsigned)) != hipSuccess ||
         hipMemset(ctx->flag, 0, 8 * sizeof(unsigned)) != hipSuccess) {
         rt_destroy(ctx);
         return RT_ERR_OUT_OF_MEMORY;
     }
+    // (best effort: without it the automatic path choice keeps the coarse kernel)
+    if (hipHostMalloc(reinterpret_cast<void**>(&ctx->od_verdict), 64, hipHostMallocDefault) ==
+        hipSuccess)
+        *ctx->od_verdict = 0u;
+    else
+        ctx->od_verdict = nullptr;
+    (void)hipGetLastError();
     // One-time setup here, as openCLInit builds the program before any trace
     // (MainState.cpp:1290-1320, outside the per-trace timer :662-894): every
     // kernel's code object is loaded onto the device now, not inside the
@@ -492,7 +518,12 @@ void rt_destroy(rt_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    // the verdict copies of rt_render_device run on the caller's streams:
+    // none may still be landing in the word (or reading flag) when it goes
+    if (ctx->verdict_copies) (void)hipDeviceSynchronize();
     if (ctx->scene_stage) (void)hipHostFree(ctx->scene_stage);
+    if (ctx->od_verdict) (void)hipHostFree(ctx->od_verdict);
+    ctx->od_verdict = nullptr;
     for (void* p : {ctx->scene_buf, ctx->origin_buf, ctx->out_buf, ctx->rec_buf, ctx->list_buf,
                     static_cast<void*>(ctx->flag)})
         if (p) (void)hipFree(p);
@@ -916,6 +947,12 @@ int rt_debug_set_coarse_waves(rt_ctx* ctx, int waves) {
     if (!ctx || !(waves == 0 || waves == 1 || waves == 2 || waves == 4 || waves == 8))
         return RT_ERR_INVALID_ARG;
     ctx->coarse_waves = waves;
+    return RT_OK;
+}
+
+int rt_debug_set_trace_bin(rt_ctx* ctx, int mode) {
+    if (!ctx || mode < 0 || mode > 2) return RT_ERR_INVALID_ARG;
+    ctx->trace_bin = mode;
     return RT_OK;
 }
 

@@ -11,7 +11,7 @@ import json
 import re
 import sys
 
-KERNEL = re.compile(r"trace\d?_kernel<0(, 0)?>")
+KERNEL = re.compile(r"trace\d?_kernel<0(, 0)?>|trace_bin_kernel<0>")
 
 
 def per_launch(path, counter):
@@ -30,7 +30,7 @@ def main(prefix, out, config=(4096, 4096, 256, 64, 3, "i32x4")):
     w, h = int(config[0]), int(config[1])
     algo = w * h * (16 if config[5] == "i32x4" else 4)
     d = {"config": [w, h, int(config[2]), int(config[3]), int(config[4]), config[5]],
-         "kernel": "trace3_kernel<0, 0>",
+         "kernel": "trace3_kernel<0, 0> / trace_bin_kernel<0>",
          "write_bytes_per_launch": write_b, "fetch_bytes_per_launch": fetch_b,
          "hbm_bytes_per_launch": write_b + fetch_b,
          "algo_bytes_per_launch": algo,

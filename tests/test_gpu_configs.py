@@ -401,6 +401,52 @@ def test_coarse_waves_exact(pkg, rt, oracle, case):
         assert np.array_equal(got, want), cw
 
 
+@pytest.mark.parametrize("case", ["ties", "cube_ties", "dense", "dense_rgba8", "band",
+                                  "wide", "nonfinite"])
+def test_trace_bin_exact(pkg, rt, oracle, case):
+    """trace_bin_kernel (no coarse kernel: each wave tile packs its bin's
+    candidates from the mask words, classifies them against itself and walks
+    the kept ones in order) gives the oracle's frame: sphere and cube ties,
+    RGBA8, a row band, the wide tile build, non-finite scene data (the
+    reference verbatim)."""
+    fmt = "rgba8" if case.endswith("rgba8") else "i32x4"
+    w, h, rows = 640, 480, (0, 480)
+    if case == "ties":
+        scene = _tie_scene(pkg, w, h, 400, 6)
+    elif case in ("cube_ties", "band"):
+        base = pkg.Scene.synthetic(w, h, 30, 60, seed=17, k=w / 640 * 3)
+        rng = np.random.default_rng(17)
+        dup = rng.choice(60, 20, replace=False)
+        cv = np.concatenate([base.cube_vertices, base.cube_vertices[dup]])
+        cc = np.concatenate([base.cube_colours, base.cube_colours[dup][:, [2, 0, 1, 3]]])
+        scene = pkg.Scene(base.sphere_origins, base.sphere_radius, base.sphere_colours, cv, cc)
+        if case == "band":
+            rows = (61, 377)
+    else:
+        scene = pkg.Scene.synthetic(w, h, 600, 30, seed=18, k=w / 640 * 4)
+        if case == "nonfinite":
+            so = np.array(scene.sphere_origins)
+            so[7, 0] = np.nan
+            scene = pkg.Scene(so, scene.sphere_radius, scene.sphere_colours,
+                              scene.cube_vertices, scene.cube_colours)
+    try:
+        rt.set_small_path(False)
+        rt.set_trace_bin(True)
+        if case == "wide":
+            rt.set_tile_variant(2)
+        got, t = rt.render(scene, w, h, rows=rows, fmt=fmt)
+        assert t.path == "binned"
+        assert rt.last_kernel() == "trace_bin_kernel"
+    finally:
+        rt.set_trace_bin(False)
+        rt.set_tile_variant(0)
+        rt.set_small_path(True)
+    want = oracle.trace(scene, w, h, rows=rows, threads=THREADS)
+    if fmt == "rgba8":
+        want = oracle.pack_rgba8(want)
+    assert np.array_equal(got, want)
+
+
 def test_render_into_registered_host_frame(pkg, rt):
     """rt_host_register: rt_render's download into a page-locked host frame
     (the app's `pixels` vector) gives the same frame, for bands too."""
@@ -484,11 +530,13 @@ def test_randomized_parity_sweep(pkg, rt, oracle, seed):
     bin_masks = bool(rng.random() < 0.75)
     split = int(rng.choice([0, 1, 2, 4]))  # waves per wave tile in the binned trace
     coarse_waves = int(rng.choice([0, 1, 2, 4, 8]))  # waves per coarse bin
+    trace_bin = int(rng.choice([0, 1, 2]))  # no coarse kernel: auto / always / never
     knobs = dict(tile=tile, small_fused=small_fused, cull_all=cull_all, bin_masks=bin_masks,
-                 split=split, coarse_waves=coarse_waves)
+                 split=split, coarse_waves=coarse_waves, trace_bin=trace_bin)
     try:
         rt.set_trace_split(split)
         rt.set_coarse_waves(coarse_waves)
+        rt.set_trace_bin(trace_bin)
         rt.set_tile_variant(tile)
         rt.set_small_fused(small_fused)
         rt.set_bin_masks(bin_masks)
@@ -500,6 +548,7 @@ def test_randomized_parity_sweep(pkg, rt, oracle, seed):
     finally:
         rt.set_trace_split(0)
         rt.set_coarse_waves(0)
+        rt.set_trace_bin(0)
         rt.set_tile_variant(0)
         rt.set_small_fused(1)
         rt.set_bin_masks(True)

@@ -807,6 +807,66 @@ def test_fresh_context_first_render(pkg):
     assert t1.kernel_us <= 3 * t2.kernel_us, (t1, t2)
 
 
+def test_trace_bin_automatic_choice(pkg, oracle):
+    """The automatic path choice (rt_debug_set_trace_bin 0): a fresh context's
+    first int32x4 frame of <= 1024 primitives above 4096 wave tiles runs prep
+    -> coarse -> trace; the coarse kernel reports the frame's box overdraw
+    to the host, and while it stays below 6 frames the next frames skip the
+    coarse kernel (trace_bin_kernel); a scene of high overdraw sends the
+    frames after the next verdict copy (the first binned launch of a context
+    and every 8th after) back to the coarse path.  RGBA8 frames keep the
+    coarse path.  Every frame is the oracle's, bit for bit.
+
+    Round 4's version of this path faulted the GPU on a fresh context's first
+    render: the page-locked verdict word was freed inside the first render's
+    staging reservation and the verdict copy then landed in the freed page.
+    The first render of a fresh context under every knob value is checked
+    first."""
+    low = pkg.Scene.synthetic(2048, 2048, 256, 64, seed=3, k=3.2)      # overdraw ~3
+    high = pkg.Scene.synthetic(2048, 2048, 256, 64, seed=3, k=12.8)    # overdraw > 6
+    want_low = oracle.trace(low, 2048, 2048, threads=THREADS)
+    want_high = oracle.trace(high, 2048, 2048, threads=THREADS)
+    for mode, first in ((0, "trace3_kernel"), (1, "trace_bin_kernel"), (2, "trace3_kernel")):
+        with pkg.RayTracer(0) as fresh:
+            fresh.set_trace_bin(mode)
+            f, _ = fresh.render(low, 2048, 2048)
+            assert fresh.last_kernel() == first, mode
+            assert np.array_equal(f, want_low), mode
+            f, _ = fresh.render(low, 2048, 2048)
+            assert fresh.last_kernel() == ("trace3_kernel" if mode == 2 else "trace_bin_kernel")
+            assert np.array_equal(f, want_low), mode
+    rt = pkg.RayTracer(0)
+    try:
+        f1, _ = rt.render(low, 2048, 2048)
+        assert rt.last_kernel() == "trace3_kernel"
+        assert np.array_equal(f1, want_low)
+        f2, _ = rt.render(low, 2048, 2048)
+        assert rt.last_kernel() == "trace_bin_kernel"
+        assert np.array_equal(f2, want_low)
+        g, _ = rt.render(low, 2048, 2048, fmt="rgba8")
+        assert rt.last_kernel() == "trace3_kernel"
+        assert np.array_equal(g, oracle.pack_rgba8(want_low))
+        # within 8 more frames the high-overdraw scene is back on the coarse
+        # path, and every frame is the oracle's
+        kernels = []
+        for _ in range(10):
+            h, _ = rt.render(high, 2048, 2048)
+            kernels.append(rt.last_kernel())
+            assert np.array_equal(h, want_high), kernels
+        assert kernels[0] == "trace_bin_kernel", kernels
+        assert kernels[-1] == "trace3_kernel", kernels
+        assert kernels.index("trace3_kernel") <= 8, kernels
+        # and a low-overdraw scene comes back to the no-coarse path
+        kernels = []
+        for _ in range(10):
+            f, _ = rt.render(low, 2048, 2048)
+            kernels.append(rt.last_kernel())
+            assert np.array_equal(f, want_low), kernels
+        assert kernels[-1] == "trace_bin_kernel", kernels
+    finally:
+        rt.close()
+
+
 def test_last_kernel_names_the_path_taken(pkg, rt, oracle):
     """rt_last_kernel reports the kernel that actually ran (the bench's
     `kernel` label): frame_small_kernel for <= 128 primitives on a resident
@@ -821,10 +881,18 @@ def test_last_kernel_names_the_path_taken(pkg, rt, oracle):
               "trace3_split_kernel"),
              (pkg.Scene.synthetic(2048, 2048, 256, 64, seed=3, k=3.2), 2048, 2048, "auto",
               "trace3_kernel"),
+             (pkg.Scene.synthetic(2048, 2048, 256, 64, seed=3, k=3.2), 2048, 2048, "bin",
+              "trace_bin_kernel"),
              (pkg.Scene.synthetic(256, 128, 8, 2, seed=1, k=0.4), 256, 128, "generic",
               "generic_kernel")]
     for scene, w, h, path, want in cases:
-        frame, _ = rt.render(scene, w, h, path=path)
+        # (binned frames of <= 1024 primitives: trace_bin_kernel forced on for
+        # "bin", off otherwise; its automatic choice is tested below)
+        rt.set_trace_bin(1 if path == "bin" else 2)
+        try:
+            frame, _ = rt.render(scene, w, h, path="auto" if path == "bin" else path)
+        finally:
+            rt.set_trace_bin(0)
         assert rt.last_kernel() == want, (w, h, scene.num_spheres, scene.num_cubes)
         if w * h <= 256 * 128:
             assert np.array_equal(frame, oracle.trace(scene, w, h))
