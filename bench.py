@@ -682,7 +682,9 @@ def run_single(args, c: Ctx, pkg):
                     "download_ms": round(best.download_us / 1e3, 3),
                     "mrays_end_to_end": round(rays / best.total_us, 1)}
         host = {"scope": "rt_render: scene upload + kernels + frame download (PCIe) into a "
-                         "reused host buffer", **host_runs(), "app": app}
+                         "reused host buffer; total_ms is the wall time of the whole call, "
+                         "upload_ms starts after the scene is packed into page-locked staging "
+                         "(rt_timing, include/rt_hip.h)", **host_runs(), "app": app}
         # the same into a page-locked buffer (rt_host_register): direct DMA
         pkg.host_register(host_buf)
         host["registered"] = host_runs()
@@ -752,7 +754,10 @@ def run_single(args, c: Ctx, pkg):
                                 "unit": "GB/s", "frac": round(t_ach / HBM_PEAK_GBS, 4),
                                 "kernel": t_kernel, "kernel_ms": round(t_trace, 4),
                                 "algo_bytes_per_launch": t_bytes,
-                                "note": "bound by per-wave test chains, not HBM (DESIGN.md §3, profiles/r02/pmc_mix)"}}
+                                # the metric's own scope: the whole frame loop
+                                "frame_frac": round(t_bytes / (t_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                "note": "bound by per-wave test chains, not HBM (DESIGN.md §3.3, "
+                                        "profiles/r04/pmc_mix_rgba8_final.txt)"}}
         del tex
 
     cpu = None if args.no_cpu_baseline else cpu_baseline(args, scene, w, h)
@@ -778,7 +783,10 @@ def run_single(args, c: Ctx, pkg):
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "kernel": kernel, "kernel_ms": round(trace_ms, 4),
                      "prep_ms": round(prep_ms, 4), "bin_ms": round(bin_ms, 4),
-                     "algo_bytes_per_launch": algo_bytes},
+                     "algo_bytes_per_launch": algo_bytes,
+                     # the frame level: the same bytes over ms_per_step (what
+                     # `value` measures: prep + binning + trace, frames in flight)
+                     "frame_frac": round(algo_bytes / (value_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
         "event_ms_per_step": round(event_ms, 4),
         "profiled_pass_ms_per_step": round(prof_wall_ms, 4),
         "clock_ramp": {"ms": args.warmup_ms, "untimed_steps": ramp_steps},
@@ -1172,9 +1180,16 @@ def multi_line(args, c: Ctx, state: dict) -> dict:
         "assembly": asm,
         "roofline": state.get("roofline"),
     }
+    rl = line["roofline"]
+    if ms and isinstance(rl, dict) and "error" not in rl:
+        # the frame level over every GPU's HBM: the assembled frame's bytes
+        # over ms_per_step against N x the one-GPU peak
+        line["roofline"] = dict(rl, frame_frac=round(
+            BYTES_PER_RAY[args.format] * w * h / (ms * 1e-3) / 1e9 / (HBM_PEAK_GBS * c.world), 4))
     for key in ("texture_rgba8", "config4", "weak_scaling", "host_frame"):
         if key in state:
             line[key] = state[key]
+    line["scaling_host_frame"] = host_frame_scaling(state.get("host_frame"))
     line["clock_ramp"] = (state.get("setup") or {}).get("clock_ramp")
     line["cpu_baseline"] = state.get("cpu_baseline")
     errors = sorted(f"{key}.{sub}" if sub else key
@@ -1184,6 +1199,23 @@ def multi_line(args, c: Ctx, state: dict) -> dict:
     if errors:
         line["phase_errors"] = errors
     return line
+
+
+def host_frame_scaling(hf) -> dict:
+    """`scaling_host_frame`: t(N=1) / t(N) of the app's host frame (the
+    `host_frame` phases: every rank fills its rows of one page-locked host
+    frame over its own PCIe link, against rank 0 alone filling it in the same
+    run and scope), per format, only for bit-exact frames (else None).  This,
+    not `value`, is the number north_star's row-tile scaling target is judged
+    by: `value` at N > 1 is the frame assembled in rank 0's
+    HBM, which no N > 1 can deliver faster than one GPU writing it locally."""
+    out = {"definition": "t(N=1)/t(N), rt_render into one shared page-locked host frame, "
+                         "same run and scope (host_frame.*.scaling)"}
+    for fmt in ("i32x4", "rgba8"):
+        e = (hf or {}).get(fmt)
+        ok = isinstance(e, dict) and e.get("frame_check") == "bit-exact" and "scaling" in e
+        out[fmt] = e["scaling"] if ok else None
+    return out
 
 
 def run_multi(args, c: Ctx, pkg):

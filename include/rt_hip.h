@@ -81,12 +81,19 @@ typedef struct rt_scene {
 typedef struct rt_timing {
     double total_us;    /* host wall time of the whole call (the reference's
                            timer scope, MainState.cpp:662-894) */
-    double upload_us;   /* H2D scene (+ origins) copy, HIP events; with
-                           explicit origins on the automatic path it also
-                           covers their on-device grid check (a small kernel,
-                           a 4-byte read-back and a stream sync before the
-                           render, so the two are serialised) */
-    double kernel_us;   /* all render kernels, HIP events */
+    double upload_us;   /* HIP events from the stream point after the scene
+                           was packed into page-locked staging on the host
+                           (that packing, a few us of memcpy, is NOT in it;
+                           it is in total_us) to the first render kernel's
+                           start: the one H2D scene DMA, the explicit-origin
+                           upload, the non-finite flag's reset when its
+                           generation wraps, and the gaps before the first
+                           kernel.  With explicit origins on the automatic
+                           path it also covers their on-device grid check (a
+                           small kernel, a 4-byte read-back and a stream sync
+                           before the render, so the two are serialised) */
+    double kernel_us;   /* first render kernel's start to the last one's end,
+                           the kernels' own dispatch-packet timestamps */
     double download_us; /* D2H frame copy, HIP events */
     int32_t path;       /* RT_PATH_BINNED or RT_PATH_GENERIC actually used */
 } rt_timing;

@@ -528,7 +528,9 @@ class RayTracer:
 
     def last_kernel(self) -> Optional[str]:
         """rt_last_kernel: the kernel the last render did its per-pixel work
-        with ("trace3_kernel", "trace_small_kernel", "frame_small_kernel",
+        with ("trace3_kernel", "trace3_split_kernel" -- the default on small
+        binned frames --, "trace_bin_kernel" -- binned frames without the
+        coarse kernel --, "trace_small_kernel", "frame_small_kernel",
         "generic_kernel"; None before any render)."""
         k = ctypes.c_int32()
         _check(library().rt_last_kernel(self._ctx, ctypes.byref(k)), "rt_last_kernel")

@@ -256,18 +256,25 @@ class HostFrame:
         return self.frame[row_begin:row_end]
 
     def close(self) -> None:
-        import torch.distributed as dist
-
-        if self.registered and self.unregister is not None:
-            self.unregister(self.frame)
-            self.registered = False
-        self.frame = None
-        if self.shm is not None:
-            self.shm.close()
-            dist.barrier(group=self.group)
-            if self.rank == self.root:
-                self.shm.unlink()
-            self.shm = None
+        """Unregister and unmap; the root unlinks the segment.  No collective:
+        POSIX keeps every other rank's mapping valid until that rank unmaps
+        it, so the root unlinks at once and a rank that failed mid-phase can
+        neither pair this with another phase's collective nor leak the
+        frame-sized /dev/shm segment (the unlink runs even if unmapping
+        raises)."""
+        try:
+            if self.registered and self.unregister is not None:
+                self.registered = False
+                self.unregister(self.frame)
+        finally:
+            self.frame = None
+            shm, self.shm = self.shm, None
+            if shm is not None:
+                try:
+                    shm.close()
+                finally:
+                    if self.rank == self.root:
+                        shm.unlink()
 
 
 def interleaved_blocks(height: int, world: int, rank: int, block: int = 64) -> List[Tuple[int, int]]:

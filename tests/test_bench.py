@@ -288,6 +288,12 @@ def _phases_worker(rank, world, port, out_path):
             ph.run("xgmi_peer_store_balanced", one_rank, state["assembly"])
             ph.run("weak_scaling", lambda: 1 / 0, state)
             ph.run("roofline", after, state)
+            # the app's host frame, one format bit-exact, one not
+            state["host_frame"] = {}
+            ph.run("i32x4", lambda: {"scaling": 1.8, "frame_check": "bit-exact"},
+                   state["host_frame"])
+            ph.run("rgba8", lambda: {"scaling": 1.5, "frame_check": "MISMATCH"},
+                   state["host_frame"])
             ph.emit()
             assert c.renewed == 3
         if rank == 0:
@@ -306,6 +312,7 @@ def test_phases_record_failures_gloo(tmp_path):
     import json
     import torch.multiprocessing as mp
 
+    b = _bench()
     out = tmp_path / "line.txt"
     mp.spawn(_phases_worker, args=(2, _free_port(), str(out)), nprocs=2, join=True)
     lines = [l for l in out.read_text().splitlines() if l.strip()]
@@ -317,7 +324,15 @@ def test_phases_record_failures_gloo(tmp_path):
     assert asm["rccl_p2p"]["frame_check"] == "bit-exact"
     # value from the one assembly that completed bit-exactly
     assert line["ms_per_step"] == 0.5 and line["value"] == pytest.approx(4096 * 4096 / 0.5e-3 / 1e6, rel=1e-3)
-    assert "error" in line["weak_scaling"] and line["roofline"] == {"frac": 0.5, "sum": 2.0}
+    assert "error" in line["weak_scaling"]
+    rl = line["roofline"]
+    assert (rl["frac"], rl["sum"]) == (0.5, 2.0)
+    # the frame level: the assembled frame's bytes over ms_per_step, N x peak
+    assert rl["frame_frac"] == pytest.approx(
+        16 * 4096 * 4096 / 0.5e-3 / 1e9 / (2 * b.HBM_PEAK_GBS), abs=1e-4)
+    # the host frame's scaling beside `value`, bit-exact formats only
+    shf = line["scaling_host_frame"]
+    assert shf["i32x4"] == 1.8 and shf["rgba8"] is None and "t(N=1)/t(N)" in shf["definition"]
     assert line["phase_errors"] == ["assembly.xgmi_peer_store",
                                     "assembly.xgmi_peer_store_balanced", "weak_scaling"]
     assert line["n_gpus"] == 2 and line["metric"]

@@ -133,7 +133,10 @@ def _host_frame_worker(rank, world, port, width, height, fmt, result_path):
         dist.barrier()  # every band is in
         if rank == 0:
             np.save(result_path, hf.frame.copy())
+        seg = "/dev/shm/" + hf.shm.name.lstrip("/")
         hf.close()
+        if rank == 0:  # the root unlinks at once, no collective in close()
+            assert not os.path.exists(seg), seg
     finally:
         dist.destroy_process_group()
 
