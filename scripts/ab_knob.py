@@ -35,6 +35,12 @@ CONFIGS = {
     "c3s16": (4096, 4096, (0, 4096), 4, 1, 1, 6.4),
     "c3": (4096, 4096, (0, 4096), 256, 64, 3, 6.4),
     "c3s": (4096, 4096, (0, 4096), 256, 64, 3, 1.0),
+    # config 3's scene with 2x / 4x / 8x the object size (box overdraw ~11 / ~45 / ~180)
+    "c3k2": (4096, 4096, (0, 4096), 256, 64, 3, 12.8),
+    "c3k4": (4096, 4096, (0, 4096), 256, 64, 3, 25.6),
+    "c3k8": (4096, 4096, (0, 4096), 256, 64, 3, 51.2),
+    # config 3's scene at 1.5x object size (overdraw ~6)
+    "c3k15": (4096, 4096, (0, 4096), 256, 64, 3, 9.6),
     "c4": (8192, 8192, (0, 8192), 192, 64, 4, 12.8),
     "c5d": (16384, 16384, (0, 16384), 4096, 0, 5, 25.6),
     "c5s": (16384, 16384, (0, 16384), 4096, 0, 5, 1.0),
@@ -58,10 +64,7 @@ CONFIGS = {
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--knob", default="coarse_cull",
-                    choices=("coarse_cull", "coarse_cull_tri", "coarse_cull_overdraw", "tile_variant",
-                             "small_fused",
-                             "small_path", "bin_masks",
-                             "trace_mode"))
+                    help="a RayTracer setter without set_ (coarse_cull, trace_bin, trace_bin_cull, ...)")
     ap.add_argument("--values", default="0,1")
     ap.add_argument("--configs", default="c3,c5d,c5s,band8")
     ap.add_argument("--format", default="i32x4", choices=("i32x4", "rgba8"))
@@ -79,20 +82,16 @@ def main():
     dev = torch.device("cuda:0")
     stream = torch.cuda.Stream(dev)
     rt = pkg.RayTracer(0)
-    setter = {"coarse_cull": rt.set_coarse_cull, "coarse_cull_tri": rt.set_coarse_cull_tri,
-              "coarse_cull_overdraw": rt.set_coarse_cull_overdraw,
-              "tile_variant": rt.set_tile_variant,
-              "small_fused": rt.set_small_fused,
-              "small_path": rt.set_small_path,
-              "bin_masks": rt.set_bin_masks, "trace_mode": rt.set_trace_mode}[args.knob]
-    setters = {"coarse_cull": rt.set_coarse_cull, "coarse_cull_tri": rt.set_coarse_cull_tri,
-               "coarse_cull_overdraw": rt.set_coarse_cull_overdraw,
-               "tile_variant": rt.set_tile_variant, "small_fused": rt.set_small_fused,
-               "small_path": rt.set_small_path, "bin_masks": rt.set_bin_masks,
-               "trace_mode": rt.set_trace_mode}
+    if args.knob == "trace_path":
+        # 0 = prep -> coarse -> trace, 1 = trace_bin_kernel (round 5 also
+        # measured 2 = trace_tile_kernel, profiles/r05/trace_tile.patch)
+        def setter(v):
+            rt.set_trace_bin({0: 2, 1: 1}[v])
+    else:
+        setter = getattr(rt, "set_" + args.knob)
     for kv in args.fixed:
         name, val = kv.split("=")
-        setters[name](int(val))
+        getattr(rt, "set_" + name)(int(val))
     values = [int(v) for v in args.values.split(",")]
     for cname in args.configs.split(","):
         w, h, (rb, re), ns, nc, seed, k = CONFIGS[cname]

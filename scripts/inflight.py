@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--knob", default=None,
                     help="RayTracer setter (without set_) applied to every slot, e.g. coarse_lds")
     ap.add_argument("--values", default="0", help="the knob's settings, interleaved")
+    ap.add_argument("--fixed", action="append", default=[],
+                    help="knob=value held on every slot for every setting (repeatable)")
     args = ap.parse_args()
     import torch
     import __graft_entry__
@@ -44,12 +46,19 @@ def main():
     outs = [torch.empty(shape, dtype=torch.int32, device=dev) for _ in range(smax)]
     fns = [ctxs[i].bind_render_device(ds, w, h, (0, h), outs[i].data_ptr(), fmt=args.format,
                                       stream=streams[i].cuda_stream) for i in range(smax)]
+    for kv in args.fixed:
+        name, val = kv.split("=")
+        for c in ctxs:
+            getattr(c, "set_" + name)(int(val))
     values = [int(v) for v in args.values.split(",")]
     res = {(v, s): [] for v in values for s in slots}
     ref = None
     for r in range(args.rounds):
         for v in values:
-            if args.knob:
+            if args.knob == "trace_path":  # as scripts/ab_knob.py
+                for c in ctxs:
+                    c.set_trace_bin({0: 2, 1: 1}[v])
+            elif args.knob:
                 for c in ctxs:
                     getattr(c, "set_" + args.knob)(v)
             for s in slots:
