@@ -92,7 +92,7 @@ def parse(argv=None):
     ap.add_argument("--trace-mode", type=int, default=0,
                     help="diagnostics ablation (needs the RT_DIAG=1 build): 1 = stores only, "
                          "2 = no per-pixel tests")
-    ap.add_argument("--pmc", default=str(REPO / "profiles" / "r04_pmc_config3.json"),
+    ap.add_argument("--pmc", default=str(REPO / "profiles" / "r05_pmc_config3.json"),
                     help="committed PMC summary to read `traffic` from")
     ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
                     help="torch.distributed backend for N>1 (nccl = RCCL over xGMI)")

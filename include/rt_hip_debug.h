@@ -76,10 +76,16 @@ int rt_debug_set_coarse_waves(rt_ctx* ctx, int waves);
 
 /* Binned frames without the coarse kernel (trace_bin_kernel: every wave tile
  * ANDs its bin's mask words and classifies the candidates itself; scenes of
- * at most 1024 primitives): 0 (default) = automatic (int32x4 frames above
- * 4096 wave tiles whose previous binned frame on this context had a box
- * overdraw below 6 frames), 1 = wherever it applies, 2 = never. */
+ * at most 1024 primitives): 0 (default) = automatic (frames above 4096 wave
+ * tiles whose previous binned frame on this context had a box overdraw below
+ * 4 frames for int32x4, 1.5 for RGBA8), 1 = wherever it applies, 2 = never. */
 int rt_debug_set_trace_bin(rt_ctx* ctx, int mode);
+
+/* The box overdraw of the last binned render of >= 1 band on this context
+ * (prep's sum of the primitives' pixel-box areas over the band's area, in
+ * frames; what the automatic path choices gate on).  Synchronises the
+ * device.  0 before any such render. */
+int rt_debug_last_overdraw(rt_ctx* ctx, double* frames);
 /* Coarse depth cull of sphere candidates in coarse bins with at least
  * `enable` sphere candidates (1 = every bin, 0 = off: every candidate the tile
  * classifier keeps stays; negative = the build's default; A/B and tests). */

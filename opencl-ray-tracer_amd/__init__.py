@@ -166,6 +166,7 @@ def library() -> ctypes.CDLL:
         "rt_debug_set_trace_split": (ctypes.c_int, [vp, ctypes.c_int]),
         "rt_debug_set_coarse_waves": (ctypes.c_int, [vp, ctypes.c_int]),
         "rt_debug_set_trace_bin": (ctypes.c_int, [vp, ctypes.c_int]),
+        "rt_debug_last_overdraw": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double)]),
         "rt_debug_triangle_t_bounds": (ctypes.c_int, [vp, vp, vp, vp, i32, i32, i32, i32, i32,
                                                       i32, i32, vp]),
         "rt_debug_triangle_box_wide": (ctypes.c_int, [vp, vp, vp, vp, i32, i32, i32, vp, vp]),
@@ -573,6 +574,14 @@ class RayTracer:
         (default), 1 = wherever it applies, 2 = never (diagnostics / tests)."""
         _check(library().rt_debug_set_trace_bin(self._ctx, int(mode)),
                "rt_debug_set_trace_bin")
+
+    def last_overdraw(self) -> float:
+        """rt_debug_last_overdraw: the last binned render's box overdraw, in
+        frames (synchronises the device)."""
+        v = ctypes.c_double()
+        _check(library().rt_debug_last_overdraw(self._ctx, ctypes.byref(v)),
+               "rt_debug_last_overdraw")
+        return v.value
 
     def set_coarse_cull_tri(self, min_candidates: int) -> None:
         """Diagnostics: triangles join the coarse depth cull in bins with at

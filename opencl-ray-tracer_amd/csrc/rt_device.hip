@@ -106,11 +106,17 @@
 #ifndef RT_COARSE_W2_BINS
 #define RT_COARSE_W2_BINS 1024  // ... with 2 waves per bin up to this many (none by default)
 #endif
-#ifndef RT_TRACE_BIN_OD
-#define RT_TRACE_BIN_OD 6  // trace_bin_kernel (auto) below this box overdraw, in frames (round 4:
-                           // config 3 (2.8) and 4096x4096 / 2560x1440 / 3840x2160 scenes of
-                           // overdraw 3-5 faster without the coarse kernel, overdraw 11+
-                           // 1.5-4x slower without its depth culls)
+#ifndef RT_TRACE_BIN_OD10
+#define RT_TRACE_BIN_OD10 40  // trace_bin_kernel (auto) for int32x4 frames below this box overdraw,
+                              // in tenths of a frame (round 5, one stream, config 3's scene scaled:
+                              // overdraw 0.08 / 0.3 / 0.7 / 1.4 / 2.8 / 4.3 / 6.1 frames, coarse path
+                              // 55.0 / 56.0 / 55.5 / 55.8 / 57.4 / 60.0 / 61.5 us per frame, no coarse
+                              // 51.3 / 51.3 / 49.6 / 49.8 / 53.9 / 60.9 / 69.2)
+#endif
+#ifndef RT_TRACE_BIN_OD10_RGBA8
+#define RT_TRACE_BIN_OD10_RGBA8 15  // ... for RGBA8 frames (same scenes: coarse path 37.5 / 39.3 /
+                                    // 40.2 / 42.0 / 44.5 / 46.7 / 47.9, no coarse 29.9 / 31.6 / 34.3 /
+                                    // 40.0 / 49.3 / 58.1 / 65.9)
 #endif
 #ifndef RT_COARSE_CULL_TRI_BINS
 #define RT_COARSE_CULL_TRI_BINS 768  // triangles join the cull only in bands of at least this
@@ -136,7 +142,8 @@ struct rt_ctx {
     void* list_buf = nullptr;   size_t list_cap = 0;    // coarse-bin candidate lists
     unsigned* flag = nullptr;   // non-finite scene flag (generation-stamped)
     // a recent binned frame's overdraw verdict (0 = none yet, 1 = below
-    // RT_TRACE_BIN_OD frames, 2 = not): the coarse or self-binning trace
+    // RT_TRACE_BIN_OD10_RGBA8 tenths of a frame, 2 = below RT_TRACE_BIN_OD10,
+    // 3 = above): the coarse or self-binning trace
     // kernel writes it to flag word 6 (device memory), and every 8th binned
     // launch copies it asynchronously into this page-locked word, which picks
     // the next int32x4 frame's path (performance only; both paths are exact)
@@ -146,6 +153,7 @@ struct rt_ctx {
     unsigned verdict_copies = 0;  // copies enqueued (rt_destroy syncs the device if any)
     unsigned gen = 0;
     unsigned od_launches = 0;  // binned launches: picks the box-overdraw slot
+    unsigned long long od_area = 0;  // the last such launch's area, 64-pixel units
     int trace_mode = 0;  // diagnostics ablation (RT_DIAG builds), see trace3_kernel
     int last_kernel = RT_KERNEL_NONE;  // the dominant kernel of the last launch (rt_last_kernel)
     int tile_variant = 0;  // 0 = by frame size, 1 = 16x16 tiles, 2 = the wide (128x2) tiles
@@ -163,8 +171,9 @@ struct rt_ctx {
     // waves per coarse bin: 0 = by band size, 1 / 2 / 4 / 8
     int coarse_waves = 0;
     // binned frames without the coarse kernel (trace_bin_kernel): 0 = auto
-    // (int32x4 frames above the split sizes whose last binned frame had a box
-    // overdraw below RT_TRACE_BIN_OD), 1 = always where it applies, 2 = never
+    // (frames above the split sizes whose last binned frame had a box
+    // overdraw below the format's threshold), 1 = always where it applies,
+    // 2 = never
     int trace_bin = 0;
     int n_cu = 256;  // compute units (rt_init)
     // coarse depth cull of sphere candidates in bins with at least this many
@@ -947,6 +956,18 @@ int rt_debug_set_coarse_waves(rt_ctx* ctx, int waves) {
     if (!ctx || !(waves == 0 || waves == 1 || waves == 2 || waves == 4 || waves == 8))
         return RT_ERR_INVALID_ARG;
     ctx->coarse_waves = waves;
+    return RT_OK;
+}
+
+int rt_debug_last_overdraw(rt_ctx* ctx, double* frames) {
+    if (!ctx || !frames) return RT_ERR_INVALID_ARG;
+    *frames = 0.0;
+    if (ctx->od_launches == 0 || ctx->od_area == 0) return RT_OK;
+    HIP_TRY(hipSetDevice(ctx->device));
+    HIP_TRY(hipDeviceSynchronize());
+    unsigned long long w[2];
+    HIP_TRY(hipMemcpy(w, ctx->flag + 2, sizeof w, hipMemcpyDeviceToHost));
+    *frames = (double)w[(ctx->od_launches - 1u) & 1u] / (double)ctx->od_area;
     return RT_OK;
 }
 

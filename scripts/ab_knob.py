@@ -41,6 +41,11 @@ CONFIGS = {
     "c3k8": (4096, 4096, (0, 4096), 256, 64, 3, 51.2),
     # config 3's scene at 1.5x object size (overdraw ~6)
     "c3k15": (4096, 4096, (0, 4096), 256, 64, 3, 9.6),
+    # ... and at 1/6.4 .. 0.7x (the RGBA8 no-coarse crossover)
+    "c3r2": (4096, 4096, (0, 4096), 256, 64, 3, 2.0),
+    "c3r3": (4096, 4096, (0, 4096), 256, 64, 3, 3.2),
+    "c3r45": (4096, 4096, (0, 4096), 256, 64, 3, 4.5),
+    "c3r8": (4096, 4096, (0, 4096), 256, 64, 3, 8.0),
     "c4": (8192, 8192, (0, 8192), 192, 64, 4, 12.8),
     "c5d": (16384, 16384, (0, 16384), 4096, 0, 5, 25.6),
     "c5s": (16384, 16384, (0, 16384), 4096, 0, 5, 1.0),
@@ -133,8 +138,10 @@ def main():
                 rt.profile(False)
                 for key in kern[v]:
                     kern[v][key].append(p[key] * 1e3 / max(p["renders"], 1))
+        step()
         res = {"config": cname, "knob": args.knob, "format": args.format, "fixed": args.fixed,
-               "frame": f"{w}x{h} rows {rb}..{re}, {ns}+{nc}, seed {seed}, k {k}"}
+               "frame": f"{w}x{h} rows {rb}..{re}, {ns}+{nc}, seed {seed}, k {k}",
+               "box_overdraw": round(rt.last_overdraw(), 3)}
         for v in values:
             res[str(v)] = {"wall_us": round(statistics.median(walls[v]), 1),
                            **{key.replace("_ms", "_us"): round(statistics.median(x), 1)
