@@ -78,7 +78,7 @@ int rt_debug_set_coarse_waves(rt_ctx* ctx, int waves);
  * ANDs its bin's mask words and classifies the candidates itself; scenes of
  * at most 1024 primitives): 0 (default) = automatic (frames above 4096 wave
  * tiles whose previous binned frame on this context had a box overdraw below
- * 4 frames for int32x4, 1.5 for RGBA8), 1 = wherever it applies, 2 = never. */
+ * 4 frames for int32x4, 1 for RGBA8), 1 = wherever it applies, 2 = never. */
 int rt_debug_set_trace_bin(rt_ctx* ctx, int mode);
 
 /* The box overdraw of the last binned render of >= 1 band on this context

@@ -114,9 +114,11 @@
                               // 51.3 / 51.3 / 49.6 / 49.8 / 53.9 / 60.9 / 69.2)
 #endif
 #ifndef RT_TRACE_BIN_OD10_RGBA8
-#define RT_TRACE_BIN_OD10_RGBA8 15  // ... for RGBA8 frames (same scenes: coarse path 37.5 / 39.3 /
+#define RT_TRACE_BIN_OD10_RGBA8 10  // ... for RGBA8 frames (same scenes: coarse path 37.5 / 39.3 /
                                     // 40.2 / 42.0 / 44.5 / 46.7 / 47.9, no coarse 29.9 / 31.6 / 34.3 /
-                                    // 40.0 / 49.3 / 58.1 / 65.9)
+                                    // 40.0 / 49.3 / 58.1 / 65.9; with 3 frames in flight at overdraw
+                                    // 0.08 / 1.4 / 2.8: coarse 18.3 / 27.5 / 32.5, no coarse 17.3 /
+                                    // 30.6 / 40.6, so 1 frame, not the one-stream crossover)
 #endif
 #ifndef RT_COARSE_CULL_TRI_BINS
 #define RT_COARSE_CULL_TRI_BINS 768  // triangles join the cull only in bands of at least this

@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--size", type=int, default=4096)
     ap.add_argument("--format", default="i32x4", choices=("i32x4", "rgba8"))
+    ap.add_argument("--k", type=float, default=None, help="object scale (default W/640: dense)")
     ap.add_argument("--knob", default=None,
                     help="RayTracer setter (without set_) applied to every slot, e.g. coarse_lds")
     ap.add_argument("--values", default="0", help="the knob's settings, interleaved")
@@ -31,7 +32,7 @@ def main():
     import __graft_entry__
     pkg = __graft_entry__.load_package()
     w = h = args.size
-    scene = pkg.Scene.synthetic(w, h, 256, 64, seed=3, k=w / 640)
+    scene = pkg.Scene.synthetic(w, h, 256, 64, seed=3, k=args.k if args.k is not None else w / 640)
     dev = torch.device("cuda:0")
     t = {n: torch.from_numpy(np.ascontiguousarray(getattr(scene, n))).to(dev)
          for n in ("sphere_origins", "sphere_radius", "sphere_colours", "cube_vertices",

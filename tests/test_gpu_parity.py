@@ -818,7 +818,7 @@ def test_trace_bin_automatic_choice(pkg, oracle):
     skip the coarse kernel (trace_bin_kernel); a scene of high overdraw sends
     the frames after the next verdict copy (the first binned launch of a
     context and every 8th after) back to the coarse path.  RGBA8 frames skip
-    the coarse kernel only below 1.5 frames (config 3's density, 2.8, keeps
+    the coarse kernel only below 1 frame (config 3's density, 2.8, keeps
     it; a sparse scene does not).  Every frame is the oracle's, bit for bit.
 
     Round 4's version of this path faulted the GPU on a fresh context's first
@@ -870,13 +870,13 @@ def test_trace_bin_automatic_choice(pkg, oracle):
         assert 2.0 < rt.last_overdraw() < 4.0, rt.last_overdraw()
     finally:
         rt.close()
-    # RGBA8 below 1.5 frames of overdraw: the Texture skips the coarse kernel too
+    # RGBA8 below 1 frame of overdraw: the Texture skips the coarse kernel too
     sparse = pkg.Scene.synthetic(2048, 2048, 256, 64, seed=5, k=0.8)
     want_sparse = oracle.pack_rgba8(oracle.trace(sparse, 2048, 2048, threads=THREADS))
     with pkg.RayTracer(0) as fresh:
         g1, _ = fresh.render(sparse, 2048, 2048, fmt="rgba8")
         assert fresh.last_kernel() == "trace3_kernel"
-        assert fresh.last_overdraw() < 1.5
+        assert fresh.last_overdraw() < 1.0
         g2, _ = fresh.render(sparse, 2048, 2048, fmt="rgba8")
         assert fresh.last_kernel() == "trace_bin_kernel"
         assert np.array_equal(g1, want_sparse) and np.array_equal(g2, want_sparse)
