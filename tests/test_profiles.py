@@ -58,8 +58,8 @@ def test_traffic_matches_pmc_passes():
                                                   REPO / "scripts" / "pmc_traffic.py")
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
-    w_kb, _ = mod.per_launch(PROF / "pmc_pass1.csv", "WRITE_SIZE")
-    f_kb, _ = mod.per_launch(PROF / "pmc_pass2.csv", "FETCH_SIZE")
+    w_kb, _, _ = mod.per_launch(PROF / "pmc_pass1.csv", "WRITE_SIZE")
+    f_kb, _, _ = mod.per_launch(PROF / "pmc_pass2.csv", "FETCH_SIZE")
     summary = json.loads((REPO / "profiles" / "r01_pmc_config3.json").read_text())
     assert summary["write_bytes_per_launch"] == int(round(w_kb * 1024))
     assert summary["fetch_bytes_per_launch"] == int(round(f_kb * 1024 * 2))
@@ -78,8 +78,8 @@ def test_config4_traffic_matches_pmc_passes():
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
     r4 = REPO / "profiles" / "r04"
-    w_kb, nw = mod.per_launch(r4 / "pmc_config4_pass1.csv", "WRITE_SIZE")
-    f_kb, nf = mod.per_launch(r4 / "pmc_config4_pass2.csv", "FETCH_SIZE")
+    w_kb, nw, _ = mod.per_launch(r4 / "pmc_config4_pass1.csv", "WRITE_SIZE")
+    f_kb, nf, _ = mod.per_launch(r4 / "pmc_config4_pass2.csv", "FETCH_SIZE")
     s = json.loads((r4 / "pmc_config4.json").read_text())
     assert s["config"] == [8192, 8192, 192, 64, 4, "i32x4"]
     assert s["write_bytes_per_launch"] == int(round(w_kb * 1024))
@@ -99,8 +99,8 @@ def test_config3_final_traffic_matches_pmc_passes():
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
     r4 = REPO / "profiles" / "r04"
-    w_kb, _ = mod.per_launch(r4 / "pmc_config3_final_pass1.csv", "WRITE_SIZE")
-    f_kb, _ = mod.per_launch(r4 / "pmc_config3_final_pass2.csv", "FETCH_SIZE")
+    w_kb, _, _ = mod.per_launch(r4 / "pmc_config3_final_pass1.csv", "WRITE_SIZE")
+    f_kb, _, _ = mod.per_launch(r4 / "pmc_config3_final_pass2.csv", "FETCH_SIZE")
     s = json.loads((REPO / "profiles" / "r04_pmc_config3.json").read_text())
     assert s["config"] == [4096, 4096, 256, 64, 3, "i32x4"]
     assert s["write_bytes_per_launch"] == int(round(w_kb * 1024))
@@ -137,3 +137,54 @@ def test_round4_other_configs_name_the_kernel_that_ran():
     assert by_size[(512, 512)] == "frame_small_kernel"      # config 1
     assert by_size[(1920, 1080)] == "frame_small_kernel"    # config 2
     assert by_size[(8192, 8192)] == "trace3_kernel"         # config 4
+
+
+def test_round5_bench_line_traffic_and_rocprof():
+    """Round 5's headline kernel (trace_bin_kernel, the no-coarse path): the
+    traffic file bench.py reads by default (profiles/r05_pmc_config3.json)
+    against the raw rows of its WRITE_SIZE / FETCH_SIZE passes (the most
+    launched trace kernel of those runs); the bench line of the same build
+    carries that traffic, both frame-level fractions, and a kernel time
+    within 5 % of rocprofv3's average over the same command (whose launches
+    also include the clock ramp and the in-flight loop)."""
+    spec = importlib.util.spec_from_file_location("pmc_traffic",
+                                                  REPO / "scripts" / "pmc_traffic.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    r5 = REPO / "profiles" / "r05"
+    w_kb, nw, kw = mod.per_launch(r5 / "pmc_config3_pass1.csv", "WRITE_SIZE")
+    f_kb, nf, kf = mod.per_launch(r5 / "pmc_config3_pass2.csv", "FETCH_SIZE")
+    assert kw == kf == "trace_bin_kernel<0>"
+    s = json.loads((REPO / "profiles" / "r05_pmc_config3.json").read_text())
+    assert s["kernel"] == "trace_bin_kernel<0>"
+    assert s["write_bytes_per_launch"] == int(round(w_kb * 1024))
+    assert s["fetch_bytes_per_launch"] == int(round(f_kb * 1024 * 2))
+    assert s["write_bytes_per_launch"] < 1.0001 * s["algo_bytes_per_launch"]
+    assert s["hbm_bytes_per_launch"] < 1.02 * s["algo_bytes_per_launch"]
+    d = json.loads((r5 / "bench_r05f.json").read_text().splitlines()[-1])
+    r = d["roofline"]
+    assert r["kernel"] == "trace_bin_kernel" and r["traffic"] == s["hbm_bytes_per_launch"]
+    assert r["frame_frac"] == pytest.approx(
+        r["algo_bytes_per_launch"] / (d["ms_per_step"] * 1e-3) / 1e9 / r["peak"], abs=2e-3)
+    t = d["texture_rgba8"]
+    assert t["roofline"]["frame_frac"] == pytest.approx(
+        t["roofline"]["algo_bytes_per_launch"] / (t["ms_per_step"] * 1e-3) / 1e9 / 8000.0,
+        abs=2e-3)
+    assert d["frames_in_flight"]["frame_check"] == "bit-exact"
+    rows = list(csv.DictReader(open(r5 / "kernel_stats_config3_r05f.csv")))
+    tb = [x for x in rows if "trace_bin_kernel<0>" in x["Name"]]
+    assert len(tb) == 1
+    assert r["kernel_ms"] == pytest.approx(float(tb[0]["AverageNs"]) / 1e6, rel=0.05)
+
+
+def test_round5_rehearsal_lines_carry_host_frame_scaling():
+    """The N = 2 / 4 rehearsal lines (ranks sharing one GPU) carry the
+    top-level scaling_host_frame of bit-exact host frames."""
+    for n in (2, 4):
+        d = json.loads((REPO / "profiles" / "r05" / f"rehearse_n{n}.json").read_text())
+        assert d["n_gpus"] == n
+        shf = d["scaling_host_frame"]
+        for fmt in ("i32x4", "rgba8"):
+            assert d["host_frame"][fmt]["frame_check"] == "bit-exact"
+            assert shf[fmt] == d["host_frame"][fmt]["scaling"]
+        assert "frame_frac" in d["roofline"]
