@@ -103,8 +103,13 @@ def parse(argv=None):
                     help="N=1: frames in flight -- step i renders frame i on slot i %% S of S "
                          "(context, stream, frame buffer) slots, so one frame's prep and "
                          "binning kernels overlap the previous frame's trace (1 = one stream)")
-    ap.add_argument("--slot-streams", default="hip", choices=("hip", "cumask", "torch"),
-                    help=argparse.SUPPRESS)  # A/B: the frames-in-flight slots' streams
+    ap.add_argument("--slot-streams", default="cumask", choices=("hip", "cumask", "torch"),
+                    help="the frames-in-flight slots' streams: cumask (default) = streams "
+                         "created with hipExtStreamCreateWithCUMask over every CU, each on a "
+                         "hardware queue of its own; hip = hipStreamCreateWithFlags; torch = "
+                         "torch's pool (round 5: RGBA8 3 slots 39.5-40.0 us per frame on hip "
+                         "streams, 33.0 on cumask, 32.8-33.8 on torch's; int32x4 2 slots "
+                         "51.1-52.0 on all three, profiles/r05/slot_streams.txt)")
     ap.add_argument("--inflight-rgba8", type=int, default=3,
                     help="the same for the texture_rgba8 leg (its trace leaves more room "
                          "beside it: 3 slots measured best, DESIGN.md §3.4)")
@@ -241,7 +246,7 @@ class Ctx:
         # the C ABI reads as "the context's own stream".
         self.stream = torch.cuda.Stream(self.dev)
         torch.cuda.set_stream(self.stream)
-        self.slot_streams = getattr(args, "slot_streams", "hip")
+        self.slot_streams = getattr(args, "slot_streams", "cumask")
 
     def renew_group(self):
         """A fresh data-path group for the phases after a failed one: a rank
@@ -465,10 +470,12 @@ def inflight_step(pkg, c: Ctx, ds, w, h, fmt, path, slots: int):
     binning kernels of one frame run beside the previous frame's trace).
     Returns (step, frames, keep-alive)."""
     rts = [pkg.RayTracer(c.gpu) for _ in range(slots)]
-    # fresh HIP streams (--slot-streams hip): torch's pool streams are handed
-    # out round-robin and may share hardware queues with streams the process
-    # made earlier, which serialises the slots
-    kind = getattr(c, "slot_streams", "hip")
+    # fresh streams of hardware queues of their own (--slot-streams cumask,
+    # every CU in the mask: hipExtStreamCreateWithCUMask always makes a new
+    # queue); plain hipStreamCreateWithFlags streams share the process's
+    # few hardware queues round-robin with streams made earlier, which
+    # serialised the RGBA8 leg's 3 slots (39.5 vs 33.0 us per frame, round 5)
+    kind = getattr(c, "slot_streams", "cumask")
     n_words = (c.torch.cuda.get_device_properties(c.dev).multi_processor_count + 31) // 32
     streams = (HipStreams(slots, n_words if kind == "cumask" else 0)
                if kind in ("hip", "cumask")
