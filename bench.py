@@ -436,7 +436,7 @@ class HipStreams:
     created now, so each takes the next hardware queue; close() destroys
     them (after a device synchronisation by the caller)."""
 
-    def __init__(self, n: int, cu_mask_words: int = 0):
+    def __init__(self, n: int, cu_mask_words: int = 0, masks=None):
         import ctypes
         self.hip = ctypes.CDLL("libamdhip64.so")
         self.hip.hipStreamCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p),
@@ -447,8 +447,9 @@ class HipStreams:
         self.handles = []
         for _ in range(n):
             st = ctypes.c_void_p()
-            if cu_mask_words:  # every CU, but a stream of its own hardware queue
-                mask = (ctypes.c_uint32 * cu_mask_words)(*([0xFFFFFFFF] * cu_mask_words))
+            if cu_mask_words:  # every CU (or masks[i]), a stream of its own hardware queue
+                words = masks[len(self.handles)] if masks else [0xFFFFFFFF] * cu_mask_words
+                mask = (ctypes.c_uint32 * cu_mask_words)(*words)
                 rc = self.hip.hipExtStreamCreateWithCUMask(ctypes.byref(st), cu_mask_words, mask)
             else:
                 rc = self.hip.hipStreamCreateWithFlags(ctypes.byref(st), 1)  # NonBlocking
