@@ -10,7 +10,7 @@
 //   rt_headless [--scene 1|2|3] [--seed S] [--width W] [--height H]
 //               [--synthetic N M k] [--rows A B] [--ppm out.ppm] [--repeat R]
 //               [--bands B] [--devices D] [--device-scene]
-//               [--format i32x4|rgba8]
+//               [--format i32x4|rgba8] [--throughput F [--inflight S]]
 //
 // --format rgba8 asks the library for the Texture's pixel format directly
 // (RT_FORMAT_RGBA8: one uint32 per pixel, bytes R, G, B, 0xFF -- the
@@ -27,10 +27,20 @@
 // scene build and no scene upload.  The printed hash must equal the host
 // build's.
 //
+// --throughput F [--inflight S] (with --synthetic, one band): the bench's
+// frame loop in C++, no Python or torch -- the scene built on the device,
+// S (context, stream, device frame) slots used round-robin, each stream
+// created with hipExtStreamCreateWithCUMask over every CU so that every
+// slot has a hardware queue of its own; untimed frames for
+// ~50 ms (the clock ramp), then F frames timed on the host clock between two
+// device synchronisations.  Prints us per frame and Grays/s, and the hash of
+// every slot's last frame (all must equal the one-frame hash).
+//
 // --bands splits [A, B) into B row bands traced concurrently through
 // rt_render_multi, one rt_ctx per band on device (band % D), each writing its
 // rows straight into the shared frame -- the reference's one pixels vector
 // (MainState.cpp:676) assembled by disjoint row ranges, SURVEY.md §8(e).
+#include <chrono>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -122,6 +132,109 @@ int render_device_scene(Band& band, int width, int height, int row_begin, int ro
     return status;
 }
 
+// --throughput: S slots round-robin over `frames` timed frames.
+int throughput(int device, int width, int height, int n, int m, unsigned seed, float k,
+               const float ray_dir[4], int32_t fmt, int frames, int slots) {
+    if (hipSetDevice(device) != hipSuccess) return 1;
+    int n_cu = 0;
+    if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
+        return 1;
+    std::vector<uint32_t> mask((size_t)(n_cu + 31) / 32, 0u);
+    for (int c = 0; c < n_cu; ++c) mask[(size_t)c / 32] |= 1u << (c % 32);
+    float *so = nullptr, *sr = nullptr, *sc = nullptr, *cv = nullptr, *cc = nullptr;
+    const size_t n4 = 4 * sizeof(float) * (size_t)(n > 0 ? n : 1);
+    const size_t m4 = 4 * sizeof(float) * (size_t)(m > 0 ? m : 1);
+    const size_t px = (size_t)width * height;
+    const size_t frame_words = (fmt == RT_FORMAT_RGBA8 ? 1 : 4) * px;
+    std::vector<rt_ctx*> ctx((size_t)slots, nullptr);
+    std::vector<hipStream_t> st((size_t)slots, nullptr);
+    std::vector<int32_t*> out((size_t)slots, nullptr);
+    int status = 1;
+    auto fail = [&](const char* what) {
+        std::fprintf(stderr, "throughput: %s failed\n", what);
+    };
+    do {
+        if (hipMalloc(&so, n4) != hipSuccess || hipMalloc(&sr, n4 / 4) != hipSuccess ||
+            hipMalloc(&sc, n4) != hipSuccess || hipMalloc(&cv, 36 * m4) != hipSuccess ||
+            hipMalloc(&cc, m4) != hipSuccess) {
+            fail("hipMalloc (scene)");
+            break;
+        }
+        bool ok = true;
+        for (int i = 0; i < slots && ok; ++i) {
+            ok = rt_init(device, &ctx[(size_t)i]) == RT_OK &&
+                 rt_reserve(ctx[(size_t)i], width, height, n, m, fmt) == RT_OK &&
+                 hipExtStreamCreateWithCUMask(&st[(size_t)i], (uint32_t)mask.size(),
+                                              mask.data()) == hipSuccess &&
+                 hipMalloc(&out[(size_t)i], frame_words * sizeof(int32_t)) == hipSuccess;
+        }
+        if (!ok) {
+            fail("slot setup");
+            break;
+        }
+        if (rt_scene_synthetic_device(ctx[0], width, height, n, m, seed, k, so, sr, sc, cv, cc,
+                                      nullptr) != RT_OK) {
+            fail("rt_scene_synthetic_device");
+            break;
+        }
+        rt_scene scene{so, sr, sc, n, cv, cc, m, nullptr, 0};
+        int f = 0;
+        auto frame = [&]() {
+            const size_t i = (size_t)(f++ % slots);
+            return rt_render_device(ctx[i], &scene, ray_dir, nullptr, width, height, 0, height,
+                                    fmt, RT_PATH_AUTO, out[i], st[i]);
+        };
+        using clk = std::chrono::steady_clock;
+        // untimed: every slot's first frames, then ~50 ms of load (the clock ramp)
+        int rc = RT_OK;
+        for (int i = 0; i < 4 * slots && rc == RT_OK; ++i) rc = frame();
+        const auto r0 = clk::now();
+        while (rc == RT_OK && clk::now() - r0 < std::chrono::milliseconds(50)) {
+            for (int i = 0; i < 16 && rc == RT_OK; ++i) rc = frame();
+            if (hipDeviceSynchronize() != hipSuccess) rc = RT_ERR_HIP;
+        }
+        if (rc != RT_OK || hipDeviceSynchronize() != hipSuccess) {
+            fail("warm-up frames");
+            break;
+        }
+        f = 0;
+        const auto t0 = clk::now();
+        for (int i = 0; i < frames && rc == RT_OK; ++i) rc = frame();
+        if (rc != RT_OK || hipDeviceSynchronize() != hipSuccess) {
+            fail("timed frames");
+            break;
+        }
+        const double us = std::chrono::duration<double, std::micro>(clk::now() - t0).count() /
+                          frames;
+        std::vector<int32_t> host(frame_words);
+        std::printf("throughput %dx%d spheres %d cubes %d %s: %d frames, %d in flight: "
+                    "%.2f us per frame, %.1f Grays/s\n",
+                    width, height, n, m, fmt == RT_FORMAT_RGBA8 ? "rgba8" : "i32x4", frames,
+                    slots, us, (double)px / us / 1e3);
+        ok = true;
+        for (int i = 0; i < slots && ok; ++i) {
+            ok = hipMemcpy(host.data(), out[(size_t)i], frame_words * sizeof(int32_t),
+                           hipMemcpyDeviceToHost) == hipSuccess;
+            if (ok)
+                std::printf("slot %d fnv1a64 %016llx\n", i,
+                            (unsigned long long)fnv1a(host.data(), host.size()));
+        }
+        int32_t kern = 0;
+        (void)rt_last_kernel(ctx[0], &kern);
+        std::printf("kernel %d\n", (int)kern);
+        status = ok ? 0 : 1;
+    } while (false);
+    (void)hipDeviceSynchronize();
+    for (int i = 0; i < slots; ++i) {
+        if (out[(size_t)i]) (void)hipFree(out[(size_t)i]);
+        if (st[(size_t)i]) (void)hipStreamDestroy(st[(size_t)i]);
+        rt_destroy(ctx[(size_t)i]);
+    }
+    for (void* p : {(void*)so, (void*)sr, (void*)sc, (void*)cv, (void*)cc})
+        if (p) (void)hipFree(p);
+    return status;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -132,6 +245,7 @@ int main(int argc, char** argv) {
     int row_begin = 0, row_end = -1;
     int n_bands = 1, n_devices = 1;
     bool device_scene = false;
+    int tp_frames = 0, tp_slots = 2;
     int32_t fmt = RT_FORMAT_I32X4;
     std::string ppm;
     for (int i = 1; i < argc; ++i) {
@@ -159,6 +273,8 @@ int main(int argc, char** argv) {
         else if (a == "--bands") n_bands = std::atoi(next());
         else if (a == "--devices") n_devices = std::atoi(next());
         else if (a == "--device-scene") device_scene = true;
+        else if (a == "--throughput") tp_frames = std::atoi(next());
+        else if (a == "--inflight") tp_slots = std::atoi(next());
         else if (a == "--format") {
             const std::string v = next();
             if (v == "i32x4") fmt = RT_FORMAT_I32X4;
@@ -182,6 +298,18 @@ int main(int argc, char** argv) {
     if (device_scene && (syn_n < 0 || n_bands != 1)) {
         std::fprintf(stderr, "--device-scene needs --synthetic and one band\n");
         return 2;
+    }
+    if (tp_frames > 0) {
+        if (syn_n < 0 || n_bands != 1 || tp_slots < 1 || tp_slots > 8 || row_begin != 0 ||
+            row_end != height) {
+            std::fprintf(stderr, "--throughput needs --synthetic, the whole frame, one band and "
+                                 "1..8 --inflight slots\n");
+            return 2;
+        }
+        float d[4];
+        rt_primary_ray_dir(d);
+        return throughput(0, width, height, syn_n, syn_m, seed, syn_k, d, fmt, tp_frames,
+                          tp_slots);
     }
 
     // Scene vectors, MainState.h:99-106 (cubes already flattened, :646-655).
