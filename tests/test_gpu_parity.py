@@ -448,6 +448,39 @@ def test_headless_cpp_driver_rgba8(pkg, oracle, scene_id, bands, tmp_path):
     assert np.all((words >> 24) == 0xff)
 
 
+@pytest.mark.parametrize("fmt,slots", [("i32x4", 2), ("rgba8", 3)])
+def test_headless_cpp_driver_throughput(pkg, oracle, fmt, slots):
+    """rt_headless --throughput: the bench's frame loop in C++ (device scene,
+    slots on CU-masked streams, the automatic path -- trace_bin_kernel for
+    int32x4 at this density) ends with every slot's last frame equal to the
+    oracle's frame (hash), and reports a positive rate."""
+    import re
+    import subprocess
+
+    exe = Path(pkg.library_path()).parent / "rt_headless"
+    if not exe.exists():
+        pytest.skip("rt_headless not built")
+    w, h = 1280, 1024
+    scene = pkg.Scene.synthetic(w, h, 256, 64, seed=3, k=w / 640)
+    want = oracle.trace(scene, w, h, threads=THREADS)
+    words = want if fmt == "i32x4" else oracle.pack_rgba8(want)
+    env = dict(os.environ)
+    env["LD_LIBRARY_PATH"] = str(exe.parent) + ":" + env.get("LD_LIBRARY_PATH", "")
+    r = subprocess.run([str(exe), "--synthetic", "256", "64", str(w / 640), "--seed", "3",
+                        "--width", str(w), "--height", str(h), "--format", fmt,
+                        "--throughput", "64", "--inflight", str(slots)],
+                       capture_output=True, text=True, env=env, timeout=120)
+    assert r.returncode == 0, r.stderr
+    hashes = re.findall(r"slot (\d+) fnv1a64 ([0-9a-f]{16})", r.stdout)
+    assert len(hashes) == slots, r.stdout
+    want_hash = oracle.fnv(np.ascontiguousarray(words).view(np.int32))
+    assert {hv for _, hv in hashes} == {f"{want_hash:016x}"}, r.stdout
+    rate = float(re.search(r"([0-9.]+) Grays/s", r.stdout).group(1))
+    assert rate > 0
+    if fmt == "i32x4":
+        assert "kernel 6" in r.stdout, r.stdout  # RT_KERNEL_TRACE_BIN
+
+
 @pytest.mark.parametrize("args", [["--synthetic", "256", "64", "6.4", "--width", "1024",
                                    "--height", "768"],
                                   ["--synthetic", "40", "5", "2", "--width", "999",
