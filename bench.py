@@ -506,6 +506,10 @@ def measure_inflight(args, c: Ctx, pkg, ds, w, h, fmt, ref_frame, slots=None):
         step()
     c.sync()
     ms = c.timed(step, args.steps)
+    # the same loop over 10 K frames: the steady-state rate, without the
+    # pipeline's fill and drain and the first dispatch after an idle GPU,
+    # which a K-frame window pays once (reported beside `value`, never it)
+    ms_long = c.timed(step, 10 * args.steps)
     same = all(bool(c.torch.equal(f, ref_frame)) for f in frames)
     c.sync()
     for rt in keep[0]:
@@ -514,6 +518,8 @@ def measure_inflight(args, c: Ctx, pkg, ds, w, h, fmt, ref_frame, slots=None):
         keep[1].close()
     return {"frames_in_flight": slots, "ms_per_step": round(ms, 4),
             "value": round(mrays_per_s(w * h, ms), 1),
+            "sustained": {"steps": 10 * args.steps, "ms_per_step": round(ms_long, 4),
+                          "value": round(mrays_per_s(w * h, ms_long), 1)},
             "frame_check": "bit-exact" if same else "MISMATCH"}
 
 
