@@ -103,6 +103,11 @@ def parse(argv=None):
                     help="N=1: frames in flight -- step i renders frame i on slot i %% S of S "
                          "(context, stream, frame buffer) slots, so one frame's prep and "
                          "binning kernels overlap the previous frame's trace (1 = one stream)")
+    ap.add_argument("--sustained", type=int, default=0,
+                    help="N=1: also time the in-flight loop over this many x K frames and "
+                         "report it as frames_in_flight.sustained (off by default: its "
+                         "overlapping launches would weigh on a rocprofv3 average of the "
+                         "default command)")
     ap.add_argument("--slot-streams", default="cumask", choices=("hip", "cumask", "torch"),
                     help="the frames-in-flight slots' streams: cumask (default) = streams "
                          "created with hipExtStreamCreateWithCUMask over every CU, each on a "
@@ -506,21 +511,24 @@ def measure_inflight(args, c: Ctx, pkg, ds, w, h, fmt, ref_frame, slots=None):
         step()
     c.sync()
     ms = c.timed(step, args.steps)
-    # the same loop over 10 K frames: the steady-state rate, without the
-    # pipeline's fill and drain and the first dispatch after an idle GPU,
-    # which a K-frame window pays once (reported beside `value`, never it)
-    ms_long = c.timed(step, 10 * args.steps)
+    out = {"frames_in_flight": slots, "ms_per_step": round(ms, 4),
+           "value": round(mrays_per_s(w * h, ms), 1)}
+    if getattr(args, "sustained", 0) > 0:
+        # the same loop over --sustained x K frames: the rate without the
+        # pipeline's fill and drain and the first dispatch after an idle GPU,
+        # which a K-frame window pays once (reported beside `value`, never it)
+        n_long = args.sustained * args.steps
+        ms_long = c.timed(step, n_long)
+        out["sustained"] = {"steps": n_long, "ms_per_step": round(ms_long, 4),
+                            "value": round(mrays_per_s(w * h, ms_long), 1)}
     same = all(bool(c.torch.equal(f, ref_frame)) for f in frames)
     c.sync()
     for rt in keep[0]:
         rt.close()
     if isinstance(keep[1], HipStreams):
         keep[1].close()
-    return {"frames_in_flight": slots, "ms_per_step": round(ms, 4),
-            "value": round(mrays_per_s(w * h, ms), 1),
-            "sustained": {"steps": 10 * args.steps, "ms_per_step": round(ms_long, 4),
-                          "value": round(mrays_per_s(w * h, ms_long), 1)},
-            "frame_check": "bit-exact" if same else "MISMATCH"}
+    out["frame_check"] = "bit-exact" if same else "MISMATCH"
+    return out
 
 
 def device_scene(pkg, c: Ctx, width, height, spheres, cubes, seed, k):
