@@ -9,13 +9,15 @@
  * once, in the reference's source order.
  *
  * Parity pinning (see DESIGN.md "Oracle"; checked by tests/test_oracle.py):
- *   - frames: the statistics SURVEY.md §0/§8c recorded from the reference's
- *     own executeRayTracerCPU, compiled and run in the survey's probe, on
- *     scenes 1-3 at 640x480 (lit-pixel count, max channel, pixels > 255,
+ *   - frames: the FNV-1a-64 known answers SURVEY.md §8c recorded from the
+ *     reference's own executeRayTracerCPU, compiled and run in the survey's
+ *     probe, on scenes 1-3 at 640x480: orc_trace's frames hash to all three
+ *     when the hash starts from 1469598103934665603 (the probe's start: the
+ *     64-bit offset basis less its last decimal digit, recovered by running
+ *     FNV-1a backwards), so every word of those frames is pinned; also the
+ *     statistics recorded there (lit-pixel count, max channel, pixels > 255,
  *     and the per-scene count / max size of the CPU-vs-OpenCL-kernel pixel
- *     differences: 33/205, 33, 0).  The survey's FNV hash strings do not
- *     reproduce under the hash definition it states; its hashing code was
- *     not recorded, so those strings are not used as a pin;
+ *     differences: 33/205, 33, 0);
  *   - cube packing: the reference's own Cube.cpp, compiled unmodified from
  *     /root/reference into oracle/_ref/libref_cube.so (oracle/Makefile),
  *     is compared vertex-for-vertex with orc_cube_* below.

@@ -11,7 +11,7 @@ sys.path.insert(0, str(REPO))
 sys.path.insert(0, str(TESTS))
 
 import __graft_entry__  # noqa: E402
-from oracle_lib import Oracle  # noqa: E402
+from oracle_lib import FNV_PRIME, PROBE_FNV_BASIS, SURVEY_FNV, Oracle, probe_fnv  # noqa: E402,F401
 
 
 def pytest_configure(config):
@@ -50,3 +50,4 @@ def load_golden(name):
 def golden_scene(pkg, g):
     return pkg.Scene(g["sphere_origins"], g["sphere_radius"], g["sphere_colours"],
                      g["cube_vertices"], g["cube_colours"])
+

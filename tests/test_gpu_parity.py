@@ -7,7 +7,7 @@ from pathlib import Path
 import numpy as np
 import pytest
 
-from conftest import GOLDEN, golden_scene, load_golden
+from conftest import GOLDEN, SURVEY_FNV, golden_scene, load_golden, probe_fnv
 
 pytestmark = pytest.mark.gpu
 
@@ -53,6 +53,18 @@ def test_golden_frame(pkg, rt, name, path):
     frame, t = rt.render(scene, w, h, ray_dir=g["ray_dir"], path=path)
     assert t.path == path
     assert not diff_report(frame, g["frame"]), diff_report(frame, g["frame"])
+
+
+@pytest.mark.parametrize("scene_id", [1, 2, 3])
+@pytest.mark.parametrize("path", ["binned", "generic"])
+def test_survey_known_answer(pkg, rt, scene_id, path):
+    """The device frame against the reference's own CPU frame as the survey's
+    probe hashed it (no oracle in the loop): the FNV-1a-64 of
+    all 1,228,800 int32 words equals the probe's known answer."""
+    g = load_golden(f"scene{scene_id}_640x480")
+    frame, t = rt.render(golden_scene(pkg, g), 640, 480, ray_dir=g["ray_dir"], path=path)
+    assert t.path == path
+    assert probe_fnv(frame) == SURVEY_FNV[scene_id]
 
 
 @pytest.mark.parametrize("name", ["scene1_640x480", "scene3_640x480", "config2_1920x1080"])
