@@ -500,7 +500,7 @@ def inflight_step(pkg, c: Ctx, ds, w, h, fmt, path, slots: int):
     return step, frames, (rts, streams)
 
 
-def measure_inflight(args, c: Ctx, pkg, ds, w, h, fmt, ref_frame, slots=None):
+def measure_inflight(args, c: Ctx, pkg, ds, w, h, fmt, ref_frame, slots=None, ramp_step=None):
     """Throughput with `slots` (default args.inflight) frames in flight (the
     N=1 `value`): the timed region is K whole frames, every one a full prep +
     bin + trace pass; each slot's frame is compared with the one-stream
@@ -509,10 +509,18 @@ def measure_inflight(args, c: Ctx, pkg, ds, w, h, fmt, ref_frame, slots=None):
     step, frames, keep = inflight_step(pkg, c, ds, w, h, fmt, args.path, slots)
     for _ in range(4 * slots + args.warmup):
         step()
-    c.sync()
+    # untimed: a clock ramp right before the window.  Setting the slots up
+    # (contexts, streams, frame buffers) leaves the GPU idle long enough for
+    # its clock to fall back, and a K = 20 window that starts there runs its
+    # first frames slow (config 3: 55-57 us per frame against 48-49 after a
+    # ramp, scripts/inflight_state.py).  The ramp runs `ramp_step` (the
+    # one-stream loop's step) when given, so that a rocprofv3 run of the
+    # bench sees these launches one at a time, as in the pass that measures
+    # the trace kernel's duration, not stretched by overlap.
+    ramp = c.clock_ramp(ramp_step or step, args.warmup_ms)
     ms = c.timed(step, args.steps)
     out = {"frames_in_flight": slots, "ms_per_step": round(ms, 4),
-           "value": round(mrays_per_s(w * h, ms), 1)}
+           "value": round(mrays_per_s(w * h, ms), 1), "clock_ramp_steps": ramp}
     if getattr(args, "sustained", 0) > 0:
         # the same loop over --sustained x K frames: the rate without the
         # pipeline's fill and drain and the first dispatch after an idle GPU,
@@ -663,7 +671,7 @@ def run_single(args, c: Ctx, pkg):
     # (a frame loop's throughput; 1 = the one-stream number above)
     inflight = None
     if args.inflight > 1 and args.trace_mode == 0:
-        inflight = measure_inflight(args, c, pkg, ds, w, h, args.format, out)
+        inflight = measure_inflight(args, c, pkg, ds, w, h, args.format, out, ramp_step=step)
     # `value`: the faster frame loop.  Frames in flight win at config 3; on
     # frames of 1 GiB and more two traces at once write the HBM less
     # efficiently than one after the other, and the one-stream loop wins
@@ -757,7 +765,8 @@ def run_single(args, c: Ctx, pkg):
         for _ in range(args.warmup):
             tstep()
         t_wall = c.timed(tstep, args.steps)
-        t_inf = (measure_inflight(args, c, pkg, ds, w, h, "rgba8", tex, args.inflight_rgba8)
+        t_inf = (measure_inflight(args, c, pkg, ds, w, h, "rgba8", tex, args.inflight_rgba8,
+                                  ramp_step=tstep)
                  if args.inflight_rgba8 > 1 else None)
         rt.profile(True)
         for _ in range(args.steps):

@@ -188,3 +188,27 @@ def test_round5_rehearsal_lines_carry_host_frame_scaling():
             assert d["host_frame"][fmt]["frame_check"] == "bit-exact"
             assert shf[fmt] == d["host_frame"][fmt]["scaling"]
         assert "frame_frac" in d["roofline"]
+
+
+def test_round5_final_bench_line_and_rocprof_launches():
+    """The final round-5 line (in-flight window after its own clock ramp):
+    its trace-kernel time within 3 % of the median launch of rocprofv3's
+    kernel trace of the same command, whose mean is the stats file's
+    AverageNs (the ramps' first launches and the in-flight windows pull
+    the mean up)."""
+    r5 = REPO / "profiles" / "r05"
+    d = json.loads((r5 / "bench_r05i.json").read_text().splitlines()[-1])
+    assert d["frames_in_flight"]["frame_check"] == "bit-exact"
+    assert d["frames_in_flight"]["clock_ramp_steps"] > 0
+    assert d["ms_per_step"] == d["frames_in_flight"]["ms_per_step"]
+    r = d["roofline"]
+    assert r["kernel"] == "trace_bin_kernel"
+    assert r["frame_frac"] == pytest.approx(
+        r["algo_bytes_per_launch"] / (d["ms_per_step"] * 1e-3) / 1e9 / r["peak"], abs=2e-3)
+    la = json.loads((r5 / "rocprof_launches_r05i.json").read_text())
+    assert r["kernel_ms"] * 1e3 == pytest.approx(la["median_us"], rel=0.03)
+    rows = list(csv.DictReader(open(r5 / "kernel_stats_config3_r05i.csv")))
+    tb = [x for x in rows if "trace_bin_kernel<0>" in x["Name"]]
+    assert len(tb) == 1 and int(tb[0]["Calls"]) == la["launches"]
+    assert float(tb[0]["AverageNs"]) / 1e3 == pytest.approx(la["mean_us"], rel=1e-3)
+
