@@ -252,6 +252,9 @@ class Ctx:
         self.stream = torch.cuda.Stream(self.dev)
         torch.cuda.set_stream(self.stream)
         self.slot_streams = getattr(args, "slot_streams", "cumask")
+        # N>1: a collective-free step (this rank's band into a private
+        # buffer) for the clock ramp before each timed window (run_multi)
+        self.ramp_step = None
 
     def renew_group(self):
         """A fresh data-path group for the phases after a failed one: a rank
@@ -1014,6 +1017,13 @@ def measure_assembly(args, c, pkg, rt, ds, width, height, fmt, how, split=False,
         return {"ms_per_step": None, "error": a.error}
     for _ in range(args.warmup):
         a.step()
+    # untimed: this rank's clock ramp (its own band into a private buffer, no
+    # collective, so the ranks need not agree on a step count) right before
+    # the window -- setting the assembly up leaves the GPU idle long enough
+    # for its clock to fall back (measure_inflight)
+    ramp_step = getattr(c, "ramp_step", None)
+    if ramp_step is not None:
+        c.clock_ramp(ramp_step, args.warmup_ms)
     c.sync()
     ms = c.timed(a.step, args.steps)
     rb0, re0 = a.bands[0]
@@ -1275,6 +1285,8 @@ def run_multi(args, c: Ctx, pkg):
                 if re > rb else (lambda: None))
         steps = c.clock_ramp(ramp, args.warmup_ms)
         c.sync()
+        env["ramp_out"] = ramp_out
+        c.ramp_step = ramp  # again right before each assembly's window
         return {"clock_ramp": {"ms": args.warmup_ms, "untimed_steps": steps}}
     phases.run("setup", setup, state)
     if "error" in state["setup"]:
@@ -1342,6 +1354,7 @@ def run_multi(args, c: Ctx, pkg):
                                           stream=c.stream.cuda_stream)
             for _ in range(args.warmup):
                 stepw()
+            c.clock_ramp(stepw, args.warmup_ms)
             wms = c.timed(stepw, args.steps)
             return {"workload": f"{w}x{hw} frame, {args.spheres * c.world} spheres + "
                                 f"{args.cubes * c.world} cubes; each rank renders {w}x{h} "
