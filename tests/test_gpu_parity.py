@@ -460,6 +460,27 @@ def test_headless_cpp_driver_rgba8(pkg, oracle, scene_id, bands, tmp_path):
     assert np.all((words >> 24) == 0xff)
 
 
+@pytest.mark.parametrize("scene_id", [1, 2, 3])
+@pytest.mark.parametrize("bands", [1, 3])
+def test_headless_known_answer(pkg, scene_id, bands):
+    """rt_headless --known-answer: the C++ host checks its frame against the
+    reference's own CPU frame as the survey's probe recorded it (SURVEY.md
+    §8c), with no Python or oracle in the loop; one band and three bands
+    (rt_render_multi) both match."""
+    import subprocess
+
+    exe = Path(pkg.library_path()).parent / "rt_headless"
+    if not exe.exists():
+        pytest.skip("rt_headless not built")
+    env = dict(os.environ)
+    env["LD_LIBRARY_PATH"] = str(exe.parent) + ":" + env.get("LD_LIBRARY_PATH", "")
+    r = subprocess.run([str(exe), "--scene", str(scene_id), "--bands", str(bands),
+                        "--known-answer"], capture_output=True, text=True, env=env, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert f"known answer scene {scene_id}: {SURVEY_FNV[scene_id]:016x}" in r.stdout, r.stdout
+    assert "match" in r.stdout and "MISMATCH" not in r.stdout
+
+
 @pytest.mark.parametrize("fmt,slots", [("i32x4", 2), ("rgba8", 3)])
 def test_headless_cpp_driver_throughput(pkg, oracle, fmt, slots):
     """rt_headless --throughput: the bench's frame loop in C++ (device scene,
