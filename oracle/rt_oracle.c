@@ -14,7 +14,10 @@
  *     probe, on scenes 1-3 at 640x480: orc_trace's frames hash to all three
  *     when the hash starts from 1469598103934665603 (the probe's start: the
  *     64-bit offset basis less its last decimal digit, recovered by running
- *     FNV-1a backwards), so every word of those frames is pinned; also the
+ *     FNV-1a backwards), so every word of those frames is pinned; the
+ *     probe's -march=native (FMA) hashes too, by this file built with FMA
+ *     contraction (liboracle_fma.so, oracle/Makefile), which pins the
+ *     expression structure at every contraction point; also the
  *     statistics recorded there (lit-pixel count, max channel, pixels > 255,
  *     and the per-scene count / max size of the CPU-vs-OpenCL-kernel pixel
  *     differences: 33/205, 33, 0);

@@ -11,7 +11,8 @@ sys.path.insert(0, str(REPO))
 sys.path.insert(0, str(TESTS))
 
 import __graft_entry__  # noqa: E402
-from oracle_lib import FNV_PRIME, PROBE_FNV_BASIS, SURVEY_FNV, Oracle, probe_fnv  # noqa: E402,F401
+from oracle_lib import (FNV_PRIME, PROBE_FNV_BASIS, SURVEY_FNV, SURVEY_FNV_FMA,  # noqa: E402,F401
+                        Oracle, probe_fnv)
 
 
 def pytest_configure(config):

@@ -18,10 +18,13 @@ probe):
     Random::getFloat() constructor arguments, which is what pins that order;
   * cube packing: the reference's unmodified Cube.cpp (oracle/_ref).
 """
+from pathlib import Path
+
 import numpy as np
 import pytest
 
-from conftest import FNV_PRIME, PROBE_FNV_BASIS, SURVEY_FNV, load_golden, probe_fnv
+from conftest import (FNV_PRIME, PROBE_FNV_BASIS, SURVEY_FNV, SURVEY_FNV_FMA, Oracle,
+                      load_golden, probe_fnv)
 from oracle_lib import ref_cube, ref_cube_lib
 
 RAY_DIR = np.array([0.0, 0.0, -1.0, -1.0], np.float32)
@@ -54,6 +57,29 @@ def test_survey_known_answers(oracle, scene_id):
     assert PROBE_FNV_BASIS == 14695981039346656037 // 10
     # the committed fixture is the same frame
     assert np.array_equal(frame, load_golden(f"scene{scene_id}_640x480")["frame"])
+
+
+def _cpu_has_fma():
+    try:
+        flags = Path("/proc/cpuinfo").read_text()
+    except OSError:
+        return False
+    return " fma " in flags and " avx2 " in flags
+
+
+@pytest.mark.skipif(not _cpu_has_fma(), reason="the FMA variant needs an x86-64-v3 CPU")
+@pytest.mark.parametrize("scene_id", [1, 2, 3])
+def test_survey_fma_known_answers(scene_id):
+    """The probe's -march=native hashes (scenes 1 and 2
+    change under FMA, scene 3 does not) from the oracle's own source built
+    with FMA contraction (liboracle_fma.so): GCC fuses a multiply into an add
+    only where one expression holds both, so these match only if the
+    restatement writes the reference's expressions -- glm's rotate and dot,
+    the Moller-Trumbore macros, the sphere test, the shade -- as the
+    reference does at every such point."""
+    fo = Oracle(fma=True)
+    frame = fo.trace(fo.scene_reference(scene_id, 1, rtl=1), 640, 480, threads=4)
+    assert probe_fnv(frame) == SURVEY_FNV_FMA[scene_id]
 
 
 def test_survey_known_answers_are_frame_sensitive(oracle):
