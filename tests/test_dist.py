@@ -70,6 +70,27 @@ def test_two_rank_row_bands_gloo(tmp_path, oracle, height, scene_id, interleave)
     assert np.array_equal(frame, want)
 
 
+@pytest.mark.parametrize("world,height,scene_id,interleave", [(4, 97, 3, 0), (8, 480, 1, 64),
+                                                             (8, 480, 2, 0)])
+def test_more_rank_row_bands_gloo(tmp_path, oracle, world, height, scene_id, interleave):
+    """The N = 4 / 8 layouts the driver's scaling run uses, rehearsed on the
+    CPU over gloo; the assembled 640x480 frames of scenes 1 and 2 are the
+    reference's own CPU frames (the survey probe's known answers)."""
+    import torch.multiprocessing as mp
+
+    from conftest import SURVEY_FNV, probe_fnv
+
+    width = 640
+    out = tmp_path / "frame.npy"
+    mp.spawn(_worker, args=(world, _free_port(), width, height, scene_id, str(out), interleave),
+             nprocs=world, join=True)
+    frame = np.load(out)
+    want = oracle.trace(oracle.scene_reference(scene_id, 1), width, height)
+    assert np.array_equal(frame, want)
+    if height == 480:
+        assert probe_fnv(frame) == SURVEY_FNV[scene_id]
+
+
 def test_band_rows_partition():
     sys.path.insert(0, str(REPO))
     import __graft_entry__
