@@ -103,11 +103,12 @@ def parse(argv=None):
                     help="N=1: frames in flight -- step i renders frame i on slot i %% S of S "
                          "(context, stream, frame buffer) slots, so one frame's prep and "
                          "binning kernels overlap the previous frame's trace (1 = one stream)")
-    ap.add_argument("--sustained", type=int, default=0,
-                    help="N=1: also time the in-flight loop over this many x K frames and "
-                         "report it as frames_in_flight.sustained (off by default: its "
-                         "overlapping launches would weigh on a rocprofv3 average of the "
-                         "default command)")
+    ap.add_argument("--sustained", type=int, default=600,
+                    help="N=1: also time the in-flight loop over this many frames (both "
+                         "formats; independent of --steps) and report it as "
+                         "frames_in_flight.sustained, the rate without a K-frame window's "
+                         "fill and drain (0 = off: for rocprofv3 runs, whose kernel average "
+                         "the long window's overlapping launches would weigh on)")
     ap.add_argument("--slot-streams", default="cumask", choices=("hip", "cumask", "torch"),
                     help="the frames-in-flight slots' streams: cumask (default) = streams "
                          "created with hipExtStreamCreateWithCUMask over every CU, each on a "
@@ -129,8 +130,13 @@ def parse(argv=None):
                     help="N>1: a phase still running after this long (a hang the collective "
                          "timeout did not end) makes rank 0 print the line so far and every "
                          "rank exit with status 3")
+    ap.add_argument("--golden", default=str(REPO / "tests" / "golden"),
+                    help="committed fixtures (data: scene arrays and frame hashes) the timed "
+                         "frame is checked against after the timed region (frame_check_ref)")
     ap.add_argument("--fail-assembly", default="",
                     help=argparse.SUPPRESS)  # tests: NAME[:RANK] raises in that assembly
+    ap.add_argument("--selftest-cpu", action="store_true",
+                    help=argparse.SUPPRESS)  # tests: the N>1 plumbing on gloo, no GPU
     return ap.parse_args(argv)
 
 
@@ -159,6 +165,41 @@ def pick_value(assemblies: dict):
         return None, None
     ms, name = min(ok)
     return name, assemblies[name]
+
+
+FIXTURE_HASH_KEYS = {"i32x4": "fnv1a64", "rgba8": "fnv1a64_rgba8"}
+SCENE_ARRAYS = ("sphere_origins", "sphere_radius", "sphere_colours", "cube_vertices",
+                "cube_colours")
+
+
+def reference_hash(scene, width: int, height: int, fmt: str, golden) -> tuple:
+    """(FNV-1a-64, fixture name) of the committed fixture for exactly this
+    workload -- same frame size and bit-identical scene arrays -- in format
+    `fmt`, or (None, why).  Fixtures are data (tests/golden/make_golden.py:
+    the oracle's frame hashed when the fixture was made), not the oracle."""
+    key = FIXTURE_HASH_KEYS[fmt]
+    for path in sorted(Path(golden).glob(f"*_{width}x{height}.npz")):
+        with np.load(path, allow_pickle=False) as z:
+            if key not in z.files or int(z["width"]) != width or int(z["height"]) != height:
+                continue
+            if all(np.array_equal(np.asarray(getattr(scene, n), np.float32).ravel(),
+                                  np.asarray(z[n], np.float32).ravel()) for n in SCENE_ARRAYS):
+                return int(z[key]), path.name
+    return None, f"no committed fixture with this {width}x{height} scene in {fmt}"
+
+
+def frame_check_ref(pkg, frame, scene, width: int, height: int, fmt: str, golden) -> dict:
+    """The timed frame against the committed fixture's hash (after the timed
+    region): {"frame_check_ref": "bit-exact" | "MISMATCH" | None, "source":
+    ...}.  `frame`: a device or host tensor / array of the whole frame."""
+    want, src = reference_hash(scene, width, height, fmt, golden)
+    if want is None:
+        return {"frame_check_ref": None, "source": src}
+    host = frame.cpu() if hasattr(frame, "cpu") else frame
+    got = pkg.fnv1a64(host)
+    return {"frame_check_ref": "bit-exact" if got == want else "MISMATCH",
+            "source": f"tests/golden/{src} {FIXTURE_HASH_KEYS[fmt]} {want:016x}",
+            "fnv1a64": f"{got:016x}"}
 
 
 def cpu_quota(root: str = "/sys/fs/cgroup"):
@@ -213,8 +254,10 @@ class Ctx:
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         local = int(os.environ.get("LOCAL_RANK", "0"))
-        if self.world != args.gpus and self.world == 1 and args.gpus != 1:
-            raise SystemExit(f"--gpus {args.gpus} needs torchrun with {args.gpus} ranks")
+        if self.world != args.gpus:
+            raise SystemExit(f"--gpus {args.gpus} with WORLD_SIZE={self.world}: the launcher "
+                             f"must start {args.gpus} ranks (or leave WORLD_SIZE unset and let "
+                             f"bench.py start them)")
         self.distributed = self.world > 1
         self.backend = "gloo" if args.rehearse else args.backend
         self.gpu = 0 if args.rehearse else local
@@ -525,13 +568,15 @@ def measure_inflight(args, c: Ctx, pkg, ds, w, h, fmt, ref_frame, slots=None, ra
     out = {"frames_in_flight": slots, "ms_per_step": round(ms, 4),
            "value": round(mrays_per_s(w * h, ms), 1), "clock_ramp_steps": ramp}
     if getattr(args, "sustained", 0) > 0:
-        # the same loop over --sustained x K frames: the rate without the
-        # pipeline's fill and drain and the first dispatch after an idle GPU,
-        # which a K-frame window pays once (reported beside `value`, never it)
-        n_long = args.sustained * args.steps
+        # the same loop over --sustained frames (a fixed count, independent
+        # of K): the rate without the pipeline's fill and drain and the first
+        # dispatch after an idle GPU, which a K-frame window pays once
+        # (reported beside `value`, never it)
+        n_long = args.sustained
         ms_long = c.timed(step, n_long)
         out["sustained"] = {"steps": n_long, "ms_per_step": round(ms_long, 4),
-                            "value": round(mrays_per_s(w * h, ms_long), 1)}
+                            "value": round(mrays_per_s(w * h, ms_long), 1),
+                            "vs_window": round(ms / ms_long, 4)}
     same = all(bool(c.torch.equal(f, ref_frame)) for f in frames)
     c.sync()
     for rt in keep[0]:
@@ -777,6 +822,9 @@ def run_single(args, c: Ctx, pkg):
         tp = rt.profile_read()
         rt.profile(False)
         t_kernel = rt.last_kernel()
+        # the Texture frame against the fixture's RGBA8 hash (the in-flight
+        # slots' frames were compared with this one-stream frame)
+        t_ref = frame_check_ref(pkg, tex, scene, w, h, "rgba8", args.golden)
         t_trace = tp["trace_ms"] / max(tp["renders"], 1)
         t_bytes = BYTES_PER_RAY["rgba8"] * w * h
         t_ach = t_bytes / (t_trace * 1e-3) / 1e9
@@ -785,6 +833,8 @@ def run_single(args, c: Ctx, pkg):
         texture = {"format": "rgba8", "ms_per_step": round(t_ms, 4),
                    "value": round(mrays_per_s(w * h, t_ms), 1), "unit": "Mrays/s",
                    "frames_in_flight": t_inf,
+                   "frame_check_ref": t_ref.pop("frame_check_ref"),
+                   "frame_check_ref_source": t_ref,
                    "one_stream": {"ms_per_step": round(t_wall, 4),
                                   "value": round(mrays_per_s(w * h, t_wall), 1)},
                    "roofline": {"bound": "hbm", "achieved": round(t_ach, 1), "peak": HBM_PEAK_GBS,
@@ -797,6 +847,9 @@ def run_single(args, c: Ctx, pkg):
                                         "profiles/r04/pmc_mix_rgba8_final.txt)"}}
         del tex
 
+    # the headline frame against the committed fixture's hash (outside every
+    # timed region; the in-flight slots' frames were compared with this one)
+    ref = frame_check_ref(pkg, out, scene, w, h, args.format, args.golden)
     cpu = None if args.no_cpu_baseline else cpu_baseline(args, scene, w, h)
     workload = CONFIG_NAMES.get((w, h, args.spheres, args.cubes), "custom")
     rt.close()
@@ -813,6 +866,8 @@ def run_single(args, c: Ctx, pkg):
                        f", {args.inflight} frames in flight (one stream, context and frame "
                        f"buffer each)" if value_ms != wall_ms else ", one stream")},
         "frames_in_flight": inflight,
+        "frame_check_ref": ref.pop("frame_check_ref"),
+        "frame_check_ref_source": ref,
         "one_stream": {"ms_per_step": round(wall_ms, 4),
                        "value": round(mrays_per_s(rays, wall_ms), 1),
                        "event_ms_per_step": round(event_ms, 4)},
@@ -972,11 +1027,13 @@ class Assembly:
         self.render_only()
         self.assemble_only()
 
-    def check(self, ds) -> str:
+    def check(self, ds, pkg=None, scene=None, golden=None) -> tuple:
         """Rank 0: the assembled frame against a one-GPU render of the whole
-        frame (bit-exact or not); broadcast so every rank agrees."""
+        frame (bit-exact or not) and, when a committed fixture holds this
+        workload (`scene` given), against the fixture's hash; broadcast so
+        every rank agrees.  Returns (frame_check, frame_check_ref)."""
         c = self.c
-        ok = c.torch.ones(1, dtype=c.torch.int32, device=c.coll_dev)
+        ok = c.torch.tensor([1, -1], dtype=c.torch.int32, device=c.coll_dev)
         if self.root:
             c.sync()
             ref = frame_tensor(c, self.height, self.width, self.fmt)
@@ -984,10 +1041,16 @@ class Assembly:
                                        ref.data_ptr(), fmt=self.fmt,
                                        stream=c.stream.cuda_stream)()
             c.sync()
-            ok.fill_(int(c.torch.equal(ref, self.frame)))
+            ok[0] = int(c.torch.equal(ref, self.frame))
             del ref
+            if scene is not None:
+                r = frame_check_ref(pkg, self.frame, scene, self.width, self.height, self.fmt,
+                                    golden)["frame_check_ref"]
+                ok[1] = -1 if r is None else int(r == "bit-exact")
         c.dist.broadcast(ok, 0, group=c.pg)
-        return "bit-exact" if int(ok.item()) else "MISMATCH"
+        ref_state = int(ok[1].item())
+        return ("bit-exact" if int(ok[0].item()) else "MISMATCH",
+                None if ref_state < 0 else "bit-exact" if ref_state else "MISMATCH")
 
     def close(self):
         if self.shared is not None:
@@ -1008,7 +1071,7 @@ def _wrap_device(c: Ctx, ptr: int, rows, width, fmt):
 
 
 def measure_assembly(args, c, pkg, rt, ds, width, height, fmt, how, split=False, bands=None,
-                     name=None):
+                     name=None, scene=None):
     if failing(args, c, name or how):
         raise RuntimeError(f"--fail-assembly {args.fail_assembly}")
     a = Assembly(c, pkg, rt, ds, width, height, fmt, how, bands=bands)
@@ -1040,7 +1103,7 @@ def measure_assembly(args, c, pkg, rt, ds, width, height, fmt, how, split=False,
             asm_ms = c.timed(a.assemble_only, args.steps)
             res["assemble_ms"] = round(asm_ms, 4)
             res["assemble_gbs_into_root"] = round(res["bytes_to_root"] / (asm_ms * 1e-3) / 1e9, 1)
-    res["frame_check"] = a.check(ds)
+    res["frame_check"], res["frame_check_ref"] = a.check(ds, pkg, scene, args.golden)
     res["rows_per_rank"] = [re - rb for rb, re in a.bands]
     a.close()
     return res
@@ -1168,7 +1231,7 @@ def device_scene_from(c: Ctx, scene):
     return t, ds
 
 
-def measure_assemblies(args, c, pkg, rt, ds, w, h, fmt, phases, res, split=False):
+def measure_assemblies(args, c, pkg, rt, ds, w, h, fmt, phases, res, split=False, scene=None):
     """The frame assembled on rank 0 three ways: equal bands by RCCL
     point-to-point, equal bands by xGMI peer stores, and cost-balanced bands
     by xGMI peer stores.  The equal split makes every other rank wait on its
@@ -1182,7 +1245,7 @@ def measure_assemblies(args, c, pkg, rt, ds, w, h, fmt, phases, res, split=False
 
     for how in ("rccl_p2p", "xgmi_peer_store"):
         phases.run(how, lambda how=how: measure_assembly(args, c, pkg, rt, ds, w, h, fmt, how,
-                                                         split=split), res)
+                                                         split=split, scene=scene), res)
 
     def balanced():
         costs = calibrate_peer_store(args, c, pkg, rt, ds, w, h, fmt)
@@ -1191,7 +1254,7 @@ def measure_assemblies(args, c, pkg, rt, ds, w, h, fmt, phases, res, split=False
                                                   "shared mapping)"}
         bal = rowbands.balanced_bands(h, costs)
         r = measure_assembly(args, c, pkg, rt, ds, w, h, fmt, "xgmi_peer_store", split=split,
-                             bands=bal, name="xgmi_peer_store_balanced")
+                             bands=bal, name="xgmi_peer_store_balanced", scene=scene)
         r["cost_model_us"] = [{"fixed": round(a * 1e6, 2), "per_row": round(s * 1e6, 4)}
                               for a, s in costs]
         return r
@@ -1230,9 +1293,11 @@ def multi_line(args, c: Ctx, state: dict) -> dict:
         # over ms_per_step against N x the one-GPU peak
         line["roofline"] = dict(rl, frame_frac=round(
             BYTES_PER_RAY[args.format] * w * h / (ms * 1e-3) / 1e9 / (HBM_PEAK_GBS * c.world), 4))
-    for key in ("texture_rgba8", "config4", "weak_scaling", "host_frame"):
+    for key in ("texture_rgba8", "config4", "weak_scaling", "host_frame", "one_gpu"):
         if key in state:
             line[key] = state[key]
+    line["frame_check_ref"] = entry.get("frame_check_ref") if entry else None
+    line.update(scaling_keys(c.world, ms, state.get("one_gpu"), state.get("weak_scaling")))
     line["scaling_host_frame"] = host_frame_scaling(state.get("host_frame"))
     line["clock_ramp"] = (state.get("setup") or {}).get("clock_ramp")
     line["cpu_baseline"] = state.get("cpu_baseline")
@@ -1243,6 +1308,30 @@ def multi_line(args, c: Ctx, state: dict) -> dict:
     if errors:
         line["phase_errors"] = errors
     return line
+
+
+SCALING_NOTE = (
+    "north_star's >= 6x row-tile scaling at 8 GPUs is read from scaling_host_frame: the app's "
+    "own consumer (pixels / the Texture's RGBA8 pixels) filled by N GPUs, each over its own "
+    "PCIe link, against one GPU filling the same buffer in the same run and scope. "
+    "scaling_assembled = t(N=1)/t(N) of `value` (the frame assembled in rank 0's HBM) cannot "
+    "reach it: 7/8 of the frame must cross xGMI into one GPU (at most 7 links x ~153 GB/s) "
+    "while one GPU writes the whole frame into its own HBM at ~6 TB/s (DESIGN.md section 7). "
+    "scaling_weak = N x t(N=1)/t(N) with every GPU rendering a frame-sized band of an N-times "
+    "taller frame.")
+
+
+def scaling_keys(world: int, ms, one_gpu, weak) -> dict:
+    """The N>1 line's scaling contract: scaling_assembled = t(N=1)/t(N) of
+    `value`'s assembly, scaling_weak = N t(N=1)/t(N) of the weak-scaling
+    frame (each rank one frame-sized band), both against rank 0 rendering
+    the whole frame alone in the same run (`one_gpu`), and the note saying
+    which number north_star's target is read from."""
+    t1 = one_gpu.get("ms_per_step") if isinstance(one_gpu, dict) else None
+    tw = weak.get("ms_per_step") if isinstance(weak, dict) else None
+    return {"scaling_assembled": round(t1 / ms, 4) if t1 and ms else None,
+            "scaling_weak": round(world * t1 / tw, 4) if t1 and tw else None,
+            "scaling_note": SCALING_NOTE}
 
 
 def host_frame_scaling(hf) -> dict:
@@ -1295,7 +1384,7 @@ def run_multi(args, c: Ctx, pkg):
     rt, ds, scene = env["rt"], env["ds"], env["scene"]
 
     measure_assemblies(args, c, pkg, rt, ds, w, h, args.format, phases, state["assembly"],
-                       split=True)
+                       split=True, scene=scene)
 
     def roofline():
         # the trace kernel on this rank's band, local stores (the roofline of
@@ -1320,10 +1409,30 @@ def run_multi(args, c: Ctx, pkg):
                 "algo_bytes_per_launch": band_bytes, "scope": "rank 0's band, local stores"}
     phases.run("roofline", roofline, state)
 
+    def one_gpu():
+        # t(N=1) in the same run, the baseline of scaling_assembled and
+        # scaling_weak: rank 0 alone renders the whole frame into a frame of
+        # its own HBM (the N=1 line's one-stream step), the others idle
+        if c.rank == 0:
+            full = frame_tensor(c, h, w, args.format)
+            step = rt.bind_render_device(ds, w, h, (0, h), full.data_ptr(), fmt=args.format,
+                                         stream=c.stream.cuda_stream)
+            for _ in range(args.warmup):
+                step()
+            c.clock_ramp(step, args.warmup_ms)
+        else:
+            step = (lambda: None)
+        ms = c.timed(step, args.steps)
+        return {"ms_per_step": round(ms, 4), "mrays": round(mrays_per_s(w * h, ms), 1),
+                "scope": "rank 0 alone renders the whole frame into its own HBM (one stream), "
+                         "same run"}
+    phases.run("one_gpu", one_gpu, state)
+
     if not args.no_extras:
         # the Texture (RGBA8, MainState.cpp:1023-1037) assembled the same way
         state["texture_rgba8"] = {}
-        measure_assemblies(args, c, pkg, rt, ds, w, h, "rgba8", phases, state["texture_rgba8"])
+        measure_assemblies(args, c, pkg, rt, ds, w, h, "rgba8", phases, state["texture_rgba8"],
+                           scene=scene)
         # BASELINE config 4: 8192^2, 192 + 64, row-tiled with the assembly
         c4 = CONFIG4
         k4 = c4["width"] / 640.0
@@ -1386,8 +1495,168 @@ def exit_status(state: dict) -> int:
     return 0 if pick_value(state.get("assembly", {}))[0] else EXIT_NO_VALUE
 
 
+# ---------------------------------------------------------------------------
+# `python bench.py --gpus N` without a launcher: one child process per rank
+# ---------------------------------------------------------------------------
+def _free_port() -> int:
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(args, argv) -> int:
+    """--gpus N > 1 with no WORLD_SIZE in the environment: start N fresh
+    processes running this script with RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_ADDR=127.0.0.1 / MASTER_PORT set -- what torchrun would do -- and
+    wait for them.  This process never touches the GPU (nothing here imports
+    torch), and it starts children rather than exec'ing over itself.  Rank
+    0's JSON line goes straight to the inherited stdout.  Exit status: 0
+    when every rank exits 0; EXIT_HUNG when a rank reports a hang (3) or has
+    to be killed because it outlived a failed rank by more than the phase
+    deadline (plus the watchdogs' grace); else the first non-zero status in
+    rank order (a signal -> 128 + its number).  SIGTERM / SIGINT are passed
+    on to the ranks.  (The reference picks one device and never starts
+    more, MainState.cpp:1241-1266.)"""
+    import signal
+    import subprocess
+
+    port = _free_port()
+    procs = []
+    base = dict(os.environ)
+    base.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    for r in range(args.gpus):
+        env = dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve()), *argv],
+                                      env=env))
+
+    def forward(signum, _frame):
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(signum)
+    old = {sig: signal.signal(sig, forward) for sig in (signal.SIGTERM, signal.SIGINT)}
+    grace = args.phase_deadline + Phases.GRACE_S + 30.0
+    failed_at, killed = None, False
+    try:
+        while any(p.poll() is None for p in procs):
+            if failed_at is None and any(p.returncode not in (None, 0) for p in procs):
+                failed_at = time.monotonic()
+            if failed_at is not None and time.monotonic() - failed_at > grace:
+                for p in procs:  # our own children, by PID
+                    if p.poll() is None:
+                        p.kill()
+                        killed = True
+            time.sleep(0.2)
+    finally:
+        for sig, h in old.items():
+            signal.signal(sig, h)
+    codes = [p.wait() for p in procs]
+    if all(rc == 0 for rc in codes):
+        return 0
+    if killed or EXIT_HUNG in codes:
+        return EXIT_HUNG
+    rc = next(rc for rc in codes if rc != 0)
+    return rc if rc > 0 else 128 - rc
+
+
+class CpuCtx(Ctx):
+    """Ctx on the CPU (--selftest-cpu): the gloo process group and the
+    barrier / timing / max-over-ranks plumbing, no device."""
+
+    def __init__(self, args):
+        import torch
+        import torch.distributed as dist
+
+        self.torch, self.dist = torch, dist
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.distributed = self.world > 1
+        self.backend = "gloo"
+        self.gpu = None
+        timeout = datetime.timedelta(seconds=max(args.init_timeout, args.pg_timeout))
+        if self.distributed:
+            dist.init_process_group("gloo", timeout=timeout)
+        self.pg_timeout = args.pg_timeout
+        self.pg = (dist.new_group(backend="gloo",
+                                  timeout=datetime.timedelta(seconds=args.pg_timeout))
+                   if self.distributed else None)
+        self.dev = self.coll_dev = torch.device("cpu")
+        self.ramp_step = None
+
+    def sync(self):
+        pass
+
+
+def run_selftest_cpu(args) -> int:
+    """The N>1 plumbing without a GPU (tests): launcher, rendezvous, phases,
+    the frame assembled on rank 0 over gloo (rowbands.assemble_frame, the
+    rccl_p2p path's collective), the one-rank baseline, weak scaling and
+    the line with its scaling keys.  Bands are filled with a known pattern
+    (pixel (y, x, c) = 1000 y + 10 x + c), not traced: no rays, no oracle."""
+    c = CpuCtx(args)
+    pkg = __graft_entry__.load_package()
+    from opencl_ray_tracer_amd import rowbands
+
+    w, h = args.width, args.height
+    torch = c.torch
+    state = {"assembly": {}}
+    phases = Phases(c, args.phase_deadline, lambda: dict(
+        multi_line(args, c, state), data="selftest: CPU pattern frame over gloo, no rays traced"),
+        args.pg_timeout)
+
+    def rows(a, b, width=w):
+        y = torch.arange(a, b, dtype=torch.int32).view(-1, 1, 1)
+        x = torch.arange(width, dtype=torch.int32).view(1, -1, 1)
+        return (1000 * y + 10 * x + torch.arange(4, dtype=torch.int32).view(1, 1, -1)).contiguous()
+
+    def assembly():
+        if failing(args, c, "rccl_p2p"):
+            raise RuntimeError(f"--fail-assembly {args.fail_assembly}")
+        rb, re = rowbands.band_rows(h, c.world, c.rank)
+        frame = torch.full((h, w, 4), -7, dtype=torch.int32) if c.rank == 0 else None
+        band = frame[rb:re] if c.rank == 0 else torch.empty((re - rb, w, 4), dtype=torch.int32)
+
+        def step():
+            band.copy_(rows(rb, re))
+            rowbands.assemble_frame(frame, band, h, c.world, c.rank, group=c.pg)
+        ms = c.timed(step, args.steps)
+        ok = torch.tensor([int(c.rank != 0 or bool(torch.equal(frame, rows(0, h))))],
+                          dtype=torch.int32)
+        c.dist.broadcast(ok, 0, group=c.pg)
+        return {"ms_per_step": round(ms, 4), "mrays": round(mrays_per_s(w * h, ms), 1),
+                "frame_check": "bit-exact" if int(ok.item()) else "MISMATCH",
+                "frame_check_ref": None,
+                "rows_per_rank": [e - b for b, e in (rowbands.band_rows(h, c.world, r)
+                                                     for r in range(c.world))]}
+    phases.run("rccl_p2p", assembly, state["assembly"])
+
+    def one_gpu():
+        full = torch.empty((h, w, 4), dtype=torch.int32)
+        step = (lambda: full.copy_(rows(0, h))) if c.rank == 0 else (lambda: None)
+        ms = c.timed(step, args.steps)
+        return {"ms_per_step": round(ms, 4), "mrays": round(mrays_per_s(w * h, ms), 1)}
+    phases.run("one_gpu", one_gpu, state)
+
+    def weak():
+        own = torch.empty((h, w, 4), dtype=torch.int32)
+        ms = c.timed(lambda: own.copy_(rows(c.rank * h, (c.rank + 1) * h)), args.steps)
+        return {"ms_per_step": round(ms, 4), "mrays": round(mrays_per_s(w * h * c.world, ms), 1)}
+    phases.run("weak_scaling", weak, state)
+    phases.emit()
+    if c.distributed:
+        c.dist.destroy_process_group()
+    return exit_status(state)
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher: start one process per rank (before any GPU call here)
+        sys.exit(launch_ranks(args, sys.argv[1:]))
+    if args.selftest_cpu:
+        sys.exit(run_selftest_cpu(args))
     c = Ctx(args)
     pkg = __graft_entry__.load_package()
     if c.distributed:

@@ -290,6 +290,15 @@ int rt_scene_synthetic_device(rt_ctx* ctx, int32_t width, int32_t height,
 /* Texture conversion (MainState.cpp:1023-1037) on the host. */
 void rt_pack_rgba8(const int32_t* frame, int64_t n_pixels, uint32_t* out);
 
+/* Known-answer checksum of a frame: FNV-1a-64 over its 32-bit words in
+ * memory order (`h ^= w; h *= 0x100000001b3`), starting from `basis`
+ * (RT_FNV1A64_BASIS; the survey's probe of the reference's CPU frames,
+ * SURVEY.md §8c, started from 1469598103934665603).  No reference
+ * counterpart: the app never checks its frame.  Used by the headless driver,
+ * the benchmark's frame check against the committed fixtures and the tests. */
+#define RT_FNV1A64_BASIS 0xcbf29ce484222325ull
+uint64_t rt_fnv1a64(const void* words, int64_t n_words, uint64_t basis);
+
 /* Library / ABI version. */
 int rt_abi_version(void);
 

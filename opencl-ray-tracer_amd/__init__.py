@@ -45,7 +45,7 @@ EXPORTED_SYMBOLS = (
     "rt_deg_to_rad", "rt_primary_ray_dir", "rt_scene_reference", "rt_scene_synthetic",
     "rt_pack_rgba8", "rt_abi_version", "rt_cube_build_device", "rt_scene_synthetic_device",
     "rt_render_multi", "rt_shared_alloc", "rt_shared_open", "rt_shared_close", "rt_shared_free",
-    "rt_host_register", "rt_host_unregister", "rt_reserve", "rt_last_kernel",
+    "rt_host_register", "rt_host_unregister", "rt_reserve", "rt_last_kernel", "rt_fnv1a64",
 )
 # rt_last_kernel's codes (RT_KERNEL_*, rt_hip.h) by name
 KERNEL_NAMES = {0: None, 1: "trace3_kernel", 2: "trace_small_kernel", 3: "frame_small_kernel",
@@ -149,6 +149,7 @@ def library() -> ctypes.CDLL:
                                               vp, vp, vp, vp]),
         "rt_pack_rgba8": (None, [vp, ctypes.c_int64, vp]),
         "rt_abi_version": (ctypes.c_int, []),
+        "rt_fnv1a64": (ctypes.c_uint64, [vp, ctypes.c_int64, ctypes.c_uint64]),
         "rt_selftest_fp32": (ctypes.c_int, [vp, vp, i32, vp, vp]),
         "rt_debug_triangle_box": (ctypes.c_int, [vp, vp, vp, vp, i32, i32, i32, vp, vp]),
         "rt_debug_sphere_box": (ctypes.c_int, [vp, f32, vp, i32, i32, i32, vp, vp]),
@@ -258,6 +259,21 @@ def pack_rgba8(frame: np.ndarray) -> np.ndarray:
     out = np.zeros(frame.shape[:-1], np.uint32)
     library().rt_pack_rgba8(_ptr(frame), n, _ptr(out))
     return out
+
+
+FNV1A64_BASIS = 0xcbf29ce484222325
+
+
+def fnv1a64(words, basis: int = FNV1A64_BASIS) -> int:
+    """FNV-1a-64 over a frame's 32-bit words in memory order (rt_fnv1a64):
+    the known-answer checksum of the committed fixtures.  `words`: a numpy
+    array (any 4-byte dtype, C-contiguous) or a CPU torch tensor."""
+    if not isinstance(words, np.ndarray):
+        words = words.contiguous().numpy()
+    words = np.ascontiguousarray(words)
+    if words.dtype.itemsize != 4:
+        raise ValueError(f"fnv1a64 hashes 32-bit words, got {words.dtype}")
+    return int(library().rt_fnv1a64(_ptr(words), words.size, basis))
 
 
 @dataclass

@@ -152,7 +152,15 @@ struct rt_ctx {
     // Its lifetime is the context's: allocated in rt_init, freed only in
     // rt_destroy after every copy into it has landed.
     unsigned* od_verdict = nullptr;
-    unsigned verdict_copies = 0;  // copies enqueued (rt_destroy syncs the device if any)
+    unsigned verdict_copies = 0;  // copies enqueued
+    // recorded behind every verdict copy: rt_destroy waits for the last one
+    // only (a context's renders move to another stream only after a
+    // synchronisation, rt_hip.h, so the last copy is the only one in flight)
+    hipEvent_t verdict_done = nullptr;
+    // rt_render: the verdict copy waits until after the frame download, so
+    // download_us times the frame alone (launch() sets verdict_due instead)
+    bool defer_verdict = false;
+    bool verdict_due = false;
     unsigned gen = 0;
     unsigned od_launches = 0;  // binned launches: picks the box-overdraw slot
     unsigned long long od_area = 0;  // the last such launch's area, 64-pixel units
@@ -285,6 +293,17 @@ int skip_k(rt_ctx* ctx, const hipEvent_t* ev) {
     return RT_OK;
 }
 
+// The overdraw verdict (flag word 6) into the context's page-locked word: a
+// 4-byte copy behind the frame's kernels on `stream`, then the context's
+// event, which rt_destroy waits for.
+int enqueue_verdict_copy(rt_ctx* ctx, hipStream_t stream) {
+    HIP_TRY(hipMemcpyAsync(ctx->od_verdict, ctx->flag + 6, sizeof(unsigned),
+                           hipMemcpyDeviceToHost, stream));
+    ++ctx->verdict_copies;
+    HIP_TRY(hipEventRecord(ctx->verdict_done, stream));
+    return RT_OK;
+}
+
 }  // namespace
 
 // The kernels and launch(), once per wave-tile shape (rt_trace.inc).
@@ -304,13 +323,18 @@ int skip_k(rt_ctx* ctx, const hipEvent_t* ev) {
 #ifndef RT_NT_WIDE
 #define RT_NT_WIDE 3
 #endif
+#ifndef RT_ROWS_NARROW
+#define RT_ROWS_NARROW 4  // pixels per lane in the 16x16 build (A/B variants: 8 = 16x32 tiles)
+#endif
 #define RT_TILE_W RT_TILE_NARROW
 #define RT_NT_STORES RT_NT_NARROW
+#define RT_ROWS RT_ROWS_NARROW
 namespace tile16 {
 #include "rt_trace.inc"
 }  // namespace tile16
 #undef RT_TILE_W
 #undef RT_NT_STORES
+#undef RT_ROWS
 #define RT_TILE_W RT_TILE_WIDE
 #define RT_NT_STORES RT_NT_WIDE
 namespace wide {
@@ -466,6 +490,10 @@ int rt_init(int device_ordinal, rt_ctx** out_ctx) {
             return RT_ERR_HIP;
         }
     }
+    if (hipEventCreateWithFlags(&ctx->verdict_done, hipEventDisableTiming) != hipSuccess) {
+        rt_destroy(ctx);
+        return RT_ERR_HIP;
+    }
     // [0] non-finite flag, [1] explicit-origin grid check, [2..5] two
     // 64-bit box-overdraw slots, [6] the overdraw verdict (see launch())
     if (hipMalloc(&ctx->flag, 8 * sizeof(unsigned)) != hipSuccess ||
@@ -530,8 +558,10 @@ void rt_destroy(rt_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     // the verdict copies of rt_render_device run on the caller's streams:
-    // none may still be landing in the word (or reading flag) when it goes
-    if (ctx->verdict_copies) (void)hipDeviceSynchronize();
+    // none may still be landing in the word (or reading flag) when it goes.
+    // The context's event follows the last one; waiting for it (not for the
+    // whole device) leaves other contexts' and other libraries' streams alone.
+    if (ctx->verdict_copies && ctx->verdict_done) (void)hipEventSynchronize(ctx->verdict_done);
     if (ctx->scene_stage) (void)hipHostFree(ctx->scene_stage);
     if (ctx->od_verdict) (void)hipHostFree(ctx->od_verdict);
     ctx->od_verdict = nullptr;
@@ -540,6 +570,7 @@ void rt_destroy(rt_ctx* ctx) {
         if (p) (void)hipFree(p);
     for (auto& e : ctx->ev)
         if (e) (void)hipEventDestroy(e);
+    if (ctx->verdict_done) (void)hipEventDestroy(ctx->verdict_done);
     for (auto e : ctx->prof_events) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -635,13 +666,22 @@ int rt_render_path(rt_ctx* ctx, const rt_scene* scene, const float ray_dir[4],
         HIP_TRY(hipEventRecord(ctx->ev[1], st));
     }
     int32_t used = 0;
+    ctx->defer_verdict = true;
+    ctx->verdict_due = false;
     rc = render_launch(ctx, &dscene, ray_dir, d_origins, width, row_begin, row_end, out_format, path,
                 ctx->out_buf, st, &used);
+    ctx->defer_verdict = false;
     ctx->span_start = ctx->span_stop = nullptr;
     if (rc) return rc;
     if (!span) HIP_TRY(hipEventRecord(ctx->ev[2], st));
     HIP_TRY(hipMemcpyAsync(host_out, ctx->out_buf, out_bytes, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipEventRecord(ctx->ev[3], st));
+    // the verdict copy after the frame's (download_us is the frame copy alone)
+    if (ctx->verdict_due) {
+        ctx->verdict_due = false;
+        rc = enqueue_verdict_copy(ctx, st);
+        if (rc) return rc;
+    }
     HIP_TRY(hipStreamSynchronize(st));
     if (timing) {
         float a = 0, b = 0, c = 0;

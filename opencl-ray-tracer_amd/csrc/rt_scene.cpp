@@ -360,6 +360,13 @@ void rt_pack_rgba8(const int32_t* frame, int64_t n_pixels, uint32_t* out) {
     }
 }
 
+uint64_t rt_fnv1a64(const void* words, int64_t n_words, uint64_t basis) {
+    const uint32_t* w = static_cast<const uint32_t*>(words);
+    uint64_t h = basis;
+    for (int64_t i = 0; i < n_words; ++i) h = (h ^ w[i]) * 0x100000001b3ull;
+    return h;
+}
+
 int rt_abi_version(void) { return RT_ABI_VERSION; }
 
 }  // extern "C"

@@ -59,12 +59,9 @@
 
 namespace {
 
-uint64_t fnv1a(const int32_t* v, size_t n, uint64_t h = 0xcbf29ce484222325ull) {
-    for (size_t i = 0; i < n; ++i) {
-        h ^= static_cast<uint32_t>(v[i]);
-        h *= 0x100000001b3ull;
-    }
-    return h;
+// FNV-1a-64 over the frame's 32-bit words (the library's rt_fnv1a64)
+uint64_t fnv1a(const int32_t* v, size_t n, uint64_t h = RT_FNV1A64_BASIS) {
+    return rt_fnv1a64(v, (int64_t)n, h);
 }
 
 // The reference's own CPU frames (MainState::executeRayTracerCPU,

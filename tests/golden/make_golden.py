@@ -56,16 +56,20 @@ def make(name, spec, oracle: Oracle, threads: int) -> None:
     frame = oracle.trace(sc, w, h, threads=threads)
     dt = time.time() - t0
     fnv = oracle.fnv(frame)
+    # the Texture packing of the same frame (MainState.cpp:1023-1037): the
+    # hash the benchmark's RGBA8 leg checks its frame against
+    fnv_rgba8 = oracle.fnv(np.ascontiguousarray(oracle.pack_rgba8(frame)).view(np.int32))
     arrays = dict(sphere_origins=sc.sphere_origins, sphere_radius=sc.sphere_radius,
                   sphere_colours=sc.sphere_colours, cube_vertices=sc.cube_vertices,
                   cube_colours=sc.cube_colours, ray_dir=oracle.ray_dir(),
                   width=np.int32(w), height=np.int32(h), fnv1a64=np.uint64(fnv),
+                  fnv1a64_rgba8=np.uint64(fnv_rgba8),
                   meta=np.array(repr(meta)))
     if store:
         arrays["frame"] = frame
     np.savez_compressed(HERE / f"{name}.npz", **arrays)
     size = (HERE / f"{name}.npz").stat().st_size
-    print(f"{name}: fnv {fnv:016x}, {dt:.1f}s oracle, {size / 1024:.0f} KiB")
+    print(f"{name}: fnv {fnv:016x} (rgba8 {fnv_rgba8:016x}), {dt:.1f}s oracle, {size / 1024:.0f} KiB")
 
 
 def main() -> None:

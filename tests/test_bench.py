@@ -516,3 +516,98 @@ def test_exit_status():
     bad = {"assembly": {"rccl_p2p": {"ms_per_step": 0.5, "frame_check": "MISMATCH"}}}
     assert b.exit_status(bad) == b.EXIT_NO_VALUE != 0
     assert b.exit_status({}) == b.EXIT_NO_VALUE
+
+
+def _launch(args, timeout):
+    import subprocess
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    return subprocess.run([sys.executable, str(REPO / "bench.py"), *args], capture_output=True,
+                          text=True, timeout=timeout, env=env)
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_bench_starts_its_own_ranks(world):
+    """`python bench.py --gpus N` with no launcher (missing #1):
+    bench.py starts N rank processes itself (RANK / WORLD_SIZE / MASTER_* set,
+    127.0.0.1, before any GPU call), and exactly one JSON line comes out, from
+    rank 0, with n_gpus N, a bit-exact assembly over gloo and the scaling
+    contract's keys (scaling_assembled, scaling_weak, scaling_note beside
+    scaling_host_frame).  --selftest-cpu: the bands are a known pattern, not
+    traced (no GPU here); the GPU rehearsal of the same launcher is in
+    tests/test_gpu_configs.py."""
+    import json
+    p = _launch(["--gpus", str(world), "--selftest-cpu", "--steps", "3", "--warmup", "1",
+                 "--width", "40", "--height", "37"], timeout=180)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [s for s in p.stdout.splitlines() if s.startswith("{")]
+    assert len(lines) == 1, p.stdout[-3000:]
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == world and line["value"] > 0
+    asm = line["assembly"]["rccl_p2p"]
+    assert asm["frame_check"] == "bit-exact" and sum(asm["rows_per_rank"]) == 37
+    t1, tn, tw = line["one_gpu"]["ms_per_step"], line["ms_per_step"], \
+        line["weak_scaling"]["ms_per_step"]
+    assert line["scaling_assembled"] == pytest.approx(t1 / tn, rel=1e-3)
+    assert line["scaling_weak"] == pytest.approx(world * t1 / tw, rel=1e-3)
+    assert "scaling_host_frame" in line["scaling_note"]
+    assert "scaling_host_frame" in line and "phase_errors" not in line
+
+
+def test_bench_own_ranks_hang_exit_status():
+    """A rank hanging inside a phase under bench.py's own launcher: the ranks'
+    watchdogs end the run, rank 0 prints one line naming the phase, and the
+    parent exits with status 3 (EXIT_HUNG), never 0."""
+    import json
+    b = _bench()
+    p = _launch(["--gpus", "2", "--selftest-cpu", "--steps", "3", "--warmup", "1", "--width", "40",
+                 "--height", "37", "--phase-deadline", "5", "--pg-timeout", "100",
+                 "--fail-assembly", "rccl_p2p:1:hang"], timeout=120)
+    assert p.returncode == b.EXIT_HUNG == 3, p.stderr[-3000:]
+    lines = [s for s in p.stdout.splitlines() if s.startswith("{")]
+    assert len(lines) == 1
+    line = json.loads(lines[0])
+    assert "timeout" in line["assembly"]["rccl_p2p"]["error"]
+    assert line["phase_errors"] == ["assembly.rccl_p2p"] and line["value"] is None
+
+
+def test_frame_check_ref_against_fixture(tmp_path):
+    """The bench's frame_check_ref (missing #2): the frame's
+    FNV-1a-64 against the committed fixture of exactly that workload (frame
+    size and scene arrays), per format; a changed word is a MISMATCH, another
+    scene has no fixture (None).  A CPU-side mock of the device frame."""
+    import __graft_entry__
+    pkg = __graft_entry__.load_package()
+    b = _bench()
+    w, h = 48, 40
+    scene = pkg.Scene.synthetic(w, h, 5, 2, seed=7, k=0.2)
+    frame = np.random.default_rng(1).integers(-300, 300, (h, w, 4)).astype(np.int32)
+    tex = pkg.pack_rgba8(frame)
+    np.savez_compressed(tmp_path / f"mock_{w}x{h}.npz", width=np.int32(w), height=np.int32(h),
+                        fnv1a64=np.uint64(pkg.fnv1a64(frame)),
+                        fnv1a64_rgba8=np.uint64(pkg.fnv1a64(tex)),
+                        **{n: getattr(scene, n) for n in b.SCENE_ARRAYS})
+    r = b.frame_check_ref(pkg, frame, scene, w, h, "i32x4", tmp_path)
+    assert r["frame_check_ref"] == "bit-exact" and f"mock_{w}x{h}.npz" in r["source"]
+    assert b.frame_check_ref(pkg, tex, scene, w, h, "rgba8", tmp_path)["frame_check_ref"] == \
+        "bit-exact"
+    bad = frame.copy()
+    bad[h - 1, w - 1, 2] += 1
+    assert b.frame_check_ref(pkg, bad, scene, w, h, "i32x4", tmp_path)["frame_check_ref"] == \
+        "MISMATCH"
+    other = pkg.Scene.synthetic(w, h, 5, 2, seed=8, k=0.2)
+    assert b.frame_check_ref(pkg, frame, other, w, h, "i32x4", tmp_path)["frame_check_ref"] is None
+    # the headline workload has its fixture, in both formats
+    a = b.parse([])
+    k = a.width / 640.0
+    c3 = pkg.Scene.synthetic(a.width, a.height, a.spheres, a.cubes, seed=a.seed, k=k)
+    for fmt in ("i32x4", "rgba8"):
+        want, src = b.reference_hash(c3, a.width, a.height, fmt, a.golden)
+        assert want is not None and src == "config3_4096x4096.npz", src
+
+
+def test_sustained_window_is_a_fixed_frame_count():
+    b = _bench()
+    a = b.parse([])
+    assert a.sustained >= 500  # default on, independent of --steps
+    assert b.parse(["--sustained", "0"]).sustained == 0

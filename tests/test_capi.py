@@ -98,3 +98,17 @@ def test_scene_helpers_validate(pkg):
     assert lib.rt_scene_reference(4, 1, None, None, None, None, None, ctypes.byref(n),
                                   ctypes.byref(n)) == -1
     assert lib.rt_scene_synthetic(0, 10, 1, 1, 1, 1.0, None, None, None, None, None) == -1
+
+
+def test_fnv1a64_helper_matches_the_fixtures(pkg, oracle):
+    """rt_fnv1a64 (the known-answer checksum the bench and the headless driver
+    use) equals the oracle's hash of every small fixture frame, and from the
+    survey probe's start it gives the reference's recorded known answers."""
+    from conftest import PROBE_FNV_BASIS, SURVEY_FNV, load_golden
+    for name in ("scene1_640x480", "scene2_640x480", "scene3_640x480", "config1_512x512"):
+        g = load_golden(name)
+        assert pkg.fnv1a64(g["frame"]) == int(g["fnv1a64"]) == oracle.fnv(g["frame"])
+        assert pkg.fnv1a64(pkg.pack_rgba8(g["frame"])) == int(g["fnv1a64_rgba8"])
+    for sid in (1, 2, 3):
+        g = load_golden(f"scene{sid}_640x480")
+        assert pkg.fnv1a64(g["frame"], PROBE_FNV_BASIS) == SURVEY_FNV[sid]

@@ -186,6 +186,58 @@ def test_bench_rehearsal_assemblies(world, tmp_path):
     # the CPU path beside the GPU numbers at N > 1 too (rank 0)
     assert line["cpu_baseline"]["value"] > 0 and line["cpu_baseline"]["cores"] >= 1
     assert "phase_errors" not in line, line.get("phase_errors")
+    # the scaling contract: against rank 0 alone in the
+    # same run; no committed fixture holds this 1024 x 512 scene
+    t1 = line["one_gpu"]["ms_per_step"]
+    assert line["scaling_assembled"] == pytest.approx(t1 / line["ms_per_step"], rel=1e-3)
+    assert line["scaling_weak"] == pytest.approx(
+        world * t1 / line["weak_scaling"]["ms_per_step"], rel=1e-3)
+    assert "scaling_host_frame" in line["scaling_note"]
+    assert line["frame_check_ref"] is None
+
+
+def _no_launcher_env():
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    return env
+
+
+def test_bench_rehearsal_without_launcher(tmp_path):
+    """`python bench.py --gpus 2` with no torchrun (missing #1):
+    bench.py starts its two ranks itself (both on cuda:0 in this rehearsal,
+    gloo), exactly one line comes out with n_gpus 2, bit-exact assemblies and
+    the scaling keys, and the status is 0."""
+    cmd = [sys.executable, str(REPO / "bench.py"), "--gpus", "2", "--rehearse", "--steps", "3",
+           "--warmup", "1", "--width", "1024", "--height", "512", "--no-extras",
+           "--no-cpu-baseline"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=_no_launcher_env(),
+                       cwd=tmp_path)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [s for s in p.stdout.splitlines() if s.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["value"] > 0
+    for how in ("rccl_p2p", "xgmi_peer_store"):
+        assert line["assembly"][how]["frame_check"] == "bit-exact", line["assembly"]
+    assert line["scaling_assembled"] == pytest.approx(
+        line["one_gpu"]["ms_per_step"] / line["ms_per_step"], rel=1e-3)
+    assert "scaling_weak" in line and "scaling_note" in line
+
+
+def test_bench_rehearsal_without_launcher_hang(tmp_path):
+    """The same with one rank hanging in an assembly: status 3 from the
+    parent, one line naming the phase."""
+    cmd = [sys.executable, str(REPO / "bench.py"), "--gpus", "2", "--rehearse", "--steps", "3",
+           "--warmup", "1", "--width", "1024", "--height", "512", "--no-extras",
+           "--no-cpu-baseline", "--pg-timeout", "300", "--phase-deadline", "20",
+           "--fail-assembly", "xgmi_peer_store:1:hang"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=110, env=_no_launcher_env(),
+                       cwd=tmp_path)
+    assert p.returncode == 3, (p.returncode, p.stderr[-3000:])
+    lines = [s for s in p.stdout.splitlines() if s.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    assert "timeout" in json.loads(lines[0])["assembly"]["xgmi_peer_store"]["error"]
 
 
 def test_bench_rehearsal_forced_failure(tmp_path):

@@ -312,25 +312,46 @@ def test_lights_do_not_change_pixels(pkg, rt):
     assert np.array_equal(rt.render(s0, 256, 200)[0], rt.render(s2, 256, 200)[0])
 
 
-def test_config3_full_frame(pkg, rt, oracle):
-    """BASELINE config 3 at full size (4096^2, 256 spheres + 64 cubes, dense):
-    the full-frame FNV-1a-64 equals the oracle's (fixture), band renders
-    assemble to the same frame, and a row sample matches the oracle."""
-    path = GOLDEN / "config3_4096x4096.npz"
-    if not path.exists():
-        pytest.skip("config3 fixture not generated")
+@pytest.mark.parametrize("trace_bin,kernel", [(1, "trace_bin_kernel"), (2, "trace3_kernel")])
+def test_config3_full_frame(pkg, oracle, trace_bin, kernel):
+    """BASELINE config 3 at full size (4096^2, 256 spheres + 64 cubes, dense),
+    the headline workload, on a FRESH context with the path pinned:
+    rt_debug_set_trace_bin 1 = prep -> trace_bin_kernel (the kernel that
+    produces the bench's `value`), 2 = prep -> coarse -> trace3_kernel.  The
+    kernel that ran is asserted, and the whole frame's FNV-1a-64 equals the
+    oracle's (tests/golden/config3_4096x4096.npz `fnv1a64`); its Texture form
+    (RGBA8, MainState.cpp:1023-1037, the bench's second leg) equals the
+    fixture's `fnv1a64_rgba8`.  On the trace_bin context, band renders
+    assemble to the same frame and a row sample matches the oracle.
+    Reference scope: MainState.cpp:858-907 (launch and readback)."""
     g = load_golden("config3_4096x4096")
     scene = golden_scene(pkg, g)
     w, h = int(g["width"]), int(g["height"])
-    frame, t = rt.render(scene, w, h)
-    assert t.path == "binned"
-    assert oracle.fnv(frame) == int(g["fnv1a64"])
-    half, _ = rt.render(scene, w, h, rows=(1000, 3000))
-    assert np.array_equal(half, frame[1000:3000])
-    rows = list(range(0, h, 256)) + [h - 1]
-    for r in rows[::4]:
-        want = oracle.trace(scene, w, h, rows=(r, r + 1))
-        assert np.array_equal(frame[r:r + 1], want), f"row {r}"
+    with pkg.RayTracer(0) as fresh:
+        fresh.set_trace_bin(trace_bin)
+        frame, t = fresh.render(scene, w, h)
+        assert t.path == "binned"
+        assert fresh.last_kernel() == kernel
+        assert pkg.fnv1a64(frame) == int(g["fnv1a64"])
+        # a second frame on the same context (after the verdict copy)
+        again, _ = fresh.render(scene, w, h)
+        assert fresh.last_kernel() == kernel
+        assert np.array_equal(again, frame)
+        del again
+        tex, _ = fresh.render(scene, w, h, fmt="rgba8")
+        # RGBA8 at this overdraw (2.8 >= 1) takes the coarse path unless forced
+        assert fresh.last_kernel() == kernel
+        assert pkg.fnv1a64(tex) == int(g["fnv1a64_rgba8"])
+        del tex
+        if trace_bin == 1:
+            half, _ = fresh.render(scene, w, h, rows=(1000, 3000))
+            assert np.array_equal(half, frame[1000:3000])
+            del half
+    if trace_bin == 1:
+        rows = list(range(0, h, 256)) + [h - 1]
+        for r in rows[::4]:
+            want = oracle.trace(scene, w, h, rows=(r, r + 1))
+            assert np.array_equal(frame[r:r + 1], want), f"row {r}"
 
 
 def test_config5_style_4096_spheres(pkg, rt, oracle):
@@ -481,32 +502,43 @@ def test_headless_known_answer(pkg, scene_id, bands):
     assert "match" in r.stdout and "MISMATCH" not in r.stdout
 
 
-@pytest.mark.parametrize("fmt,slots", [("i32x4", 2), ("rgba8", 3)])
-def test_headless_cpp_driver_throughput(pkg, oracle, fmt, slots):
+@pytest.mark.parametrize("fmt,slots,w,h", [("i32x4", 2, 1280, 1024), ("rgba8", 3, 1280, 1024),
+                                          ("rgba8", 2, 1280, 1024), ("i32x4", 2, 4096, 4096),
+                                          ("rgba8", 2, 4096, 4096)])
+def test_headless_cpp_driver_throughput(pkg, oracle, fmt, slots, w, h):
     """rt_headless --throughput: the bench's frame loop in C++ (device scene,
     slots on CU-masked streams, the automatic path -- trace_bin_kernel for
     int32x4 at this density) ends with every slot's last frame equal to the
-    oracle's frame (hash), and reports a positive rate."""
+    oracle's frame (hash), and reports a positive rate.  At 4096^2 (BASELINE
+    config 3, the headline workload: the loop that produces `value`, 2
+    CU-masked slots) the hash is the committed fixture's
+    (tests/golden/config3_4096x4096.npz fnv1a64 / fnv1a64_rgba8)."""
     import re
     import subprocess
 
     exe = Path(pkg.library_path()).parent / "rt_headless"
     if not exe.exists():
         pytest.skip("rt_headless not built")
-    w, h = 1280, 1024
-    scene = pkg.Scene.synthetic(w, h, 256, 64, seed=3, k=w / 640)
-    want = oracle.trace(scene, w, h, threads=THREADS)
-    words = want if fmt == "i32x4" else oracle.pack_rgba8(want)
+    if (w, h) == (4096, 4096):
+        g = load_golden("config3_4096x4096")
+        want_hash = int(g["fnv1a64" if fmt == "i32x4" else "fnv1a64_rgba8"])
+        frames = "400"
+    else:
+        scene = pkg.Scene.synthetic(w, h, 256, 64, seed=3, k=w / 640)
+        want = oracle.trace(scene, w, h, threads=THREADS)
+        words = want if fmt == "i32x4" else oracle.pack_rgba8(want)
+        want_hash = oracle.fnv(np.ascontiguousarray(words).view(np.int32))
+        frames = "64"
     env = dict(os.environ)
     env["LD_LIBRARY_PATH"] = str(exe.parent) + ":" + env.get("LD_LIBRARY_PATH", "")
     r = subprocess.run([str(exe), "--synthetic", "256", "64", str(w / 640), "--seed", "3",
                         "--width", str(w), "--height", str(h), "--format", fmt,
-                        "--throughput", "64", "--inflight", str(slots)],
+                        "--throughput", frames, "--inflight", str(slots)],
                        capture_output=True, text=True, env=env, timeout=120)
     assert r.returncode == 0, r.stderr
+    print(r.stdout)
     hashes = re.findall(r"slot (\d+) fnv1a64 ([0-9a-f]{16})", r.stdout)
     assert len(hashes) == slots, r.stdout
-    want_hash = oracle.fnv(np.ascontiguousarray(words).view(np.int32))
     assert {hv for _, hv in hashes} == {f"{want_hash:016x}"}, r.stdout
     rate = float(re.search(r"([0-9.]+) Grays/s", r.stdout).group(1))
     assert rate > 0
@@ -839,9 +871,9 @@ def test_first_render_is_not_cold(tmp_path):
     """The one-time setup is rt_init's (openCLInit's place, MainState.cpp:
     1290-1320, outside the trace timer :662-894): in a fresh process, the
     first rt_render of reference scene 1 at 640x480 on the first context
-    spends under 1 ms of kernel time (code objects loaded in rt_init,
-    workspace reserved before the timed events; the first/second ratio is a
-    bench record, not asserted here), and every frame is the golden frame."""
+    spends at most 20x a warm call's kernel time (at least 250 us, at most
+    1 ms; code objects loaded in rt_init, workspace reserved before the timed
+    events), and every frame is the golden frame."""
     import json
     import subprocess
     import sys
@@ -855,10 +887,12 @@ def test_first_render_is_not_cold(tmp_path):
     print("first / second / third kernel_us:", [round(c["kernel_us"], 1) for c in calls])
     assert all(c["ok"] for c in calls)
     assert kernel == "frame_small_kernel"
-    # an absolute bound that only a cold code-object load or an allocation
-    # inside the kernel span can break (round 3 measured 2.7 ms for those;
-    # warm calls take ~10 us): no timing ratio on a shared, clock-ramping box
-    assert calls[0]["kernel_us"] < 1000.0, calls
+    # a bound that a cold code-object load or an allocation inside the kernel
+    # span breaks (round 3 measured 2.7 ms for those; warm calls take ~10 us,
+    # the first 12-13 us): 20x the warm calls, at least 250 us (a fresh box's
+    # clock ramp), never above 1 ms
+    warm = min(c["kernel_us"] for c in calls[1:])
+    assert calls[0]["kernel_us"] < min(1000.0, max(250.0, 20.0 * warm)), calls
 
 
 def test_fresh_context_first_render(pkg):
@@ -873,7 +907,8 @@ def test_fresh_context_first_render(pkg):
         ok1 = np.array_equal(out, g["frame"])
         _, t2 = fresh.render(scene, 640, 480, out=out)
     assert ok1 and np.array_equal(out, g["frame"])
-    assert t1.kernel_us < 1000.0, (t1, t2)  # (see test_first_render_is_not_cold)
+    # (see test_first_render_is_not_cold)
+    assert t1.kernel_us < min(1000.0, max(250.0, 20.0 * t2.kernel_us)), (t1, t2)
 
 
 def test_trace_bin_automatic_choice(pkg, oracle):
