@@ -7,6 +7,7 @@ import importlib.util
 import json
 from pathlib import Path
 
+import numpy as np
 import pytest
 
 REPO = Path(__file__).resolve().parents[1]
@@ -212,3 +213,25 @@ def test_round5_final_bench_line_and_rocprof_launches():
     assert len(tb) == 1 and int(tb[0]["Calls"]) == la["launches"]
     assert float(tb[0]["AverageNs"]) / 1e3 == pytest.approx(la["mean_us"], rel=1e-3)
 
+
+
+def test_round6_bench_line_checks_its_frames_against_the_fixture():
+    """Round 6's line (profiles/r06/bench_r06a.json, the default command on
+    the box): both formats' timed frames equal the committed fixture's hash
+    (frame_check_ref), the long in-flight window is on by default (600
+    frames, independent of --steps) for both formats, and the int32x4 window
+    agrees with it within 5 % (the Texture's 3-slot K = 20 window pays the
+    pipeline's fill and drain)."""
+    d = json.loads((REPO / "profiles" / "r06" / "bench_r06a.json").read_text().splitlines()[-1])
+    g = np.load(REPO / "tests" / "golden" / "config3_4096x4096.npz")
+    assert d["frame_check_ref"] == "bit-exact"
+    assert d["frame_check_ref_source"]["fnv1a64"] == f"{int(g['fnv1a64']):016x}"
+    t = d["texture_rgba8"]
+    assert t["frame_check_ref"] == "bit-exact"
+    assert t["frame_check_ref_source"]["fnv1a64"] == f"{int(g['fnv1a64_rgba8']):016x}"
+    for leg in (d, t):
+        s = leg["frames_in_flight"]["sustained"]
+        assert s["steps"] == 600
+        assert s["vs_window"] == pytest.approx(leg["frames_in_flight"]["ms_per_step"] /
+                                               s["ms_per_step"], rel=5e-3)
+    assert d["frames_in_flight"]["sustained"]["vs_window"] == pytest.approx(1.0, abs=0.05)
