@@ -92,7 +92,7 @@ def parse(argv=None):
     ap.add_argument("--trace-mode", type=int, default=0,
                     help="diagnostics ablation (needs the RT_DIAG=1 build): 1 = stores only, "
                          "2 = no per-pixel tests")
-    ap.add_argument("--pmc", default=str(REPO / "profiles" / "r05_pmc_config3.json"),
+    ap.add_argument("--pmc", default=str(REPO / "profiles" / "r06_pmc_config3.json"),
                     help="committed PMC summary to read `traffic` from")
     ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
                     help="torch.distributed backend for N>1 (nccl = RCCL over xGMI)")
@@ -138,6 +138,28 @@ def parse(argv=None):
     ap.add_argument("--selftest-cpu", action="store_true",
                     help=argparse.SUPPRESS)  # tests: the N>1 plumbing on gloo, no GPU
     return ap.parse_args(argv)
+
+
+# The ONE JSON line goes to the process's original stdout; everything else
+# written to fd 1 (C/C++ libraries' logging, e.g. gloo's "[Gloo] Rank ...
+# connected" lines at N > 1) is sent to stderr by claim_stdout().
+_LINE_OUT = None
+
+
+def claim_stdout():
+    global _LINE_OUT
+    if _LINE_OUT is not None:
+        return
+    sys.stdout.flush()
+    fd = os.dup(1)
+    os.dup2(2, 1)
+    _LINE_OUT = os.fdopen(fd, "w", buffering=1)
+
+
+def emit_line(text: str):
+    out = _LINE_OUT if _LINE_OUT is not None else sys.stdout
+    out.write(text + "\n")
+    out.flush()
 
 
 # ---------------------------------------------------------------------------
@@ -439,7 +461,7 @@ class Phases:
                 time.sleep(0.05)
                 text = json.dumps({"metric": METRIC, "value": None, "unit": "Mrays/s",
                                    "n_gpus": self.c.world, "error": f"line: {e!r}"})
-        print(text, flush=True)
+        emit_line(text)
 
     def agree(self, ok: bool) -> bool:
         if self.ctrl is None:
@@ -1655,6 +1677,7 @@ def main():
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # no launcher: start one process per rank (before any GPU call here)
         sys.exit(launch_ranks(args, sys.argv[1:]))
+    claim_stdout()
     if args.selftest_cpu:
         sys.exit(run_selftest_cpu(args))
     c = Ctx(args)
@@ -1664,7 +1687,7 @@ def main():
         c.dist.destroy_process_group()
         sys.exit(status)
     line = run_single(args, c, pkg)
-    print(json.dumps(line), flush=True)
+    emit_line(json.dumps(line))
 
 
 if __name__ == "__main__":

@@ -540,8 +540,10 @@ def test_bench_starts_its_own_ranks(world):
     p = _launch(["--gpus", str(world), "--selftest-cpu", "--steps", "3", "--warmup", "1",
                  "--width", "40", "--height", "37"], timeout=180)
     assert p.returncode == 0, p.stderr[-3000:]
-    lines = [s for s in p.stdout.splitlines() if s.startswith("{")]
-    assert len(lines) == 1, p.stdout[-3000:]
+    # stdout is the line and nothing else (gloo's "[Gloo] Rank ..." logging
+    # and any other fd-1 output go to stderr)
+    lines = [s for s in p.stdout.splitlines() if s.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), p.stdout[-3000:]
     line = json.loads(lines[0])
     assert line["n_gpus"] == world and line["value"] > 0
     asm = line["assembly"]["rccl_p2p"]
