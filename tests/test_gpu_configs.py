@@ -189,9 +189,10 @@ def test_bench_rehearsal_assemblies(world, tmp_path):
     # the scaling contract: against rank 0 alone in the
     # same run; no committed fixture holds this 1024 x 512 scene
     t1 = line["one_gpu"]["ms_per_step"]
-    assert line["scaling_assembled"] == pytest.approx(t1 / line["ms_per_step"], rel=1e-3)
+    assert line["scaling_assembled"] == pytest.approx(t1 / line["ms_per_step"], rel=1e-3,
+                                                      abs=1e-4)
     assert line["scaling_weak"] == pytest.approx(
-        world * t1 / line["weak_scaling"]["ms_per_step"], rel=1e-3)
+        world * t1 / line["weak_scaling"]["ms_per_step"], rel=1e-3, abs=1e-4)
     assert "scaling_host_frame" in line["scaling_note"]
     assert line["frame_check_ref"] is None
 
@@ -221,7 +222,7 @@ def test_bench_rehearsal_without_launcher(tmp_path):
     for how in ("rccl_p2p", "xgmi_peer_store"):
         assert line["assembly"][how]["frame_check"] == "bit-exact", line["assembly"]
     assert line["scaling_assembled"] == pytest.approx(
-        line["one_gpu"]["ms_per_step"] / line["ms_per_step"], rel=1e-3)
+        line["one_gpu"]["ms_per_step"] / line["ms_per_step"], rel=1e-3, abs=1e-4)
     assert "scaling_weak" in line and "scaling_note" in line
 
 

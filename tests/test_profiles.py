@@ -235,3 +235,23 @@ def test_round6_bench_line_checks_its_frames_against_the_fixture():
         assert s["vs_window"] == pytest.approx(leg["frames_in_flight"]["ms_per_step"] /
                                                s["ms_per_step"], rel=5e-3)
     assert d["frames_in_flight"]["sustained"]["vs_window"] == pytest.approx(1.0, abs=0.05)
+
+
+def test_round6_rehearsal_lines_carry_the_scaling_contract():
+    """The N = 2 / 4 / 8 rehearsals of round 6 (bench.py starting its own
+    ranks, every rank on one GPU, gloo): every assembly bit-exact against the
+    one-GPU render AND the committed fixture's hash, and the line's scaling
+    keys consistent with its own timings."""
+    for n in (2, 4, 8):
+        d = json.loads((REPO / "profiles" / "r06" / f"rehearse_n{n}.json").read_text())
+        assert d["n_gpus"] == n and "phase_errors" not in d
+        for how, a in d["assembly"].items():
+            assert a["frame_check"] == "bit-exact" and a["frame_check_ref"] == "bit-exact", how
+        assert d["frame_check_ref"] == "bit-exact"
+        t1 = d["one_gpu"]["ms_per_step"]
+        assert d["scaling_assembled"] == pytest.approx(t1 / d["ms_per_step"], rel=1e-3, abs=1e-4)
+        assert d["scaling_weak"] == pytest.approx(n * t1 / d["weak_scaling"]["ms_per_step"],
+                                                  rel=1e-3, abs=1e-4)
+        assert "scaling_host_frame" in d["scaling_note"]
+        for fmt in ("i32x4", "rgba8"):
+            assert d["host_frame"][fmt]["frame_check"] == "bit-exact"
