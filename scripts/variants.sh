@@ -6,7 +6,7 @@ set -e
 R="$(cd "$(dirname "$0")/.." && pwd)"
 C="$R/opencl-ray-tracer_amd/csrc"; V="$R/opencl-ray-tracer_amd/variants"
 mkdir -p "$V"
-HIPFLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -I$R/include"
+HIPFLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -mllvm -amdgpu-kernarg-preload-count=16 -I$R/include"
 make -s -C "$C" rt_scene.o rt_scene_device.o rt_args.o
 pids=()
 for spec in "$@"; do
