@@ -276,7 +276,7 @@ def test_round6_final_line_agrees_with_rocprof_and_pmc():
     assert len(tb) == 1 and float(tb[0]["AverageNs"]) / 1e3 == pytest.approx(la["mean_us"], rel=1e-3)
     pmc = json.loads((REPO / "profiles" / "r06_pmc_config3.json").read_text())
     # (the line read the PMC file committed before this run: the previous
-    # passes over the same kernel code, 18 KB of fetch apart)
+    # library's passes, 18 KB of fetch apart)
     assert r["traffic"] == pytest.approx(pmc["hbm_bytes_per_launch"], rel=1e-3)
     assert pmc["hbm_bytes_per_launch"] / pmc["algo_bytes_per_launch"] == pytest.approx(1.011, abs=2e-3)
     assert r["frac"] == pytest.approx(
