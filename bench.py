@@ -599,6 +599,11 @@ def measure_inflight(args, c: Ctx, pkg, ds, w, h, fmt, ref_frame, slots=None, ra
         out["sustained"] = {"steps": n_long, "ms_per_step": round(ms_long, 4),
                             "value": round(mrays_per_s(w * h, ms_long), 1),
                             "vs_window": round(ms / ms_long, 4)}
+        if abs(ms / ms_long - 1.0) > 0.05:
+            out["sustained"]["note"] = (
+                f"the K = {args.steps} window with {slots} slots pays the pipeline's fill and "
+                f"drain once (its first frames start on an idle GPU, its last drain alone); "
+                f"over {n_long} frames that is amortised (DESIGN.md section 3.4)")
     same = all(bool(c.torch.equal(f, ref_frame)) for f in frames)
     c.sync()
     for rt in keep[0]:
