@@ -257,21 +257,22 @@ def test_round6_rehearsal_lines_carry_the_scaling_contract():
             assert d["host_frame"][fmt]["frame_check"] == "bit-exact"
 
 
-def test_round6_final_line_agrees_with_rocprof_and_pmc():
-    """The final round-6 line (profiles/r06/bench_r06k_final.json): the trace
+@pytest.mark.parametrize("tag", ["r06k_final", "r06m_final"])
+def test_round6_final_line_agrees_with_rocprof_and_pmc(tag):
+    """The final round-6 lines (profiles/r06/bench_<tag>.json): the trace
     kernel's time from its packet events within 5 % of rocprofv3's mean over
     the same command (--sustained 0) and 2 % of its median; the line's
     traffic equals the committed PMC passes (1.011x the frame, no re-reads);
     both formats' frames equal the fixture."""
     r6 = REPO / "profiles" / "r06"
-    d = json.loads((r6 / "bench_r06k_final.json").read_text().splitlines()[-1])
+    d = json.loads((r6 / f"bench_{tag}.json").read_text().splitlines()[-1])
     r = d["roofline"]
     assert r["kernel"] == "trace_bin_kernel" and d["frame_check_ref"] == "bit-exact"
     assert d["texture_rgba8"]["frame_check_ref"] == "bit-exact"
-    la = json.loads((r6 / "rocprof_launches_r06k_final.json").read_text())
+    la = json.loads((r6 / f"rocprof_launches_{tag}.json").read_text())
     assert r["kernel_ms"] * 1e3 == pytest.approx(la["mean_us"], rel=0.05)
     assert r["kernel_ms"] * 1e3 == pytest.approx(la["median_us"], rel=0.02)
-    rows = list(csv.DictReader(open(r6 / "kernel_stats_config3_r06k_final.csv")))
+    rows = list(csv.DictReader(open(r6 / f"kernel_stats_config3_{tag}.csv")))
     tb = [x for x in rows if "trace_bin_kernel<0>" in x["Name"]]
     assert len(tb) == 1 and float(tb[0]["AverageNs"]) / 1e3 == pytest.approx(la["mean_us"], rel=1e-3)
     pmc = json.loads((REPO / "profiles" / "r06_pmc_config3.json").read_text())
