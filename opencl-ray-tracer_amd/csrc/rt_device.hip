@@ -120,6 +120,10 @@
                                     // 0.08 / 1.4 / 2.8: coarse 18.3 / 27.5 / 32.5, no coarse 17.3 /
                                     // 30.6 / 40.6, so 1 frame, not the one-stream crossover)
 #endif
+#ifndef RT_VERDICT_DIRECT
+#define RT_VERDICT_DIRECT 1  // the kernels write the overdraw verdict into the host word themselves
+                             // (every binned launch, no copy; rt_ctx::od_verdict)
+#endif
 #ifndef RT_COARSE_CULL_TRI_BINS
 #define RT_COARSE_CULL_TRI_BINS 768  // triangles join the cull only in bands of at least this
                                      // many coarse bins: fewer coarse waves run as one
@@ -145,13 +149,16 @@ struct rt_ctx {
     unsigned* flag = nullptr;   // non-finite scene flag (generation-stamped)
     // a recent binned frame's overdraw verdict (0 = none yet, 1 = below
     // RT_TRACE_BIN_OD10_RGBA8 tenths of a frame, 2 = below RT_TRACE_BIN_OD10,
-    // 3 = above): the coarse or self-binning trace
-    // kernel writes it to flag word 6 (device memory), and every 8th binned
-    // launch copies it asynchronously into this page-locked word, which picks
-    // the next int32x4 frame's path (performance only; both paths are exact)
+    // 3 = above): the coarse or self-binning trace kernel writes it straight
+    // into this page-locked, device-mapped word (od_verdict_dev, a
+    // system-scope store, every binned launch: RT_VERDICT_DIRECT), or, where
+    // that mapping is unavailable, to flag word 6 (device memory), which
+    // every 8th binned launch copies asynchronously into the word.  The word
+    // picks the next frame's path (performance only; both paths are exact).
     // Its lifetime is the context's: allocated in rt_init, freed only in
-    // rt_destroy after every copy into it has landed.
+    // rt_destroy after every write into it has landed.
     unsigned* od_verdict = nullptr;
+    unsigned* od_verdict_dev = nullptr;  // its device mapping (direct writes), or null
     unsigned verdict_copies = 0;  // copies enqueued
     // recorded behind every verdict copy: rt_destroy waits for the last one
     // only (a context's renders move to another stream only after a
@@ -501,12 +508,19 @@ int rt_init(int device_ordinal, rt_ctx** out_ctx) {
         rt_destroy(ctx);
         return RT_ERR_OUT_OF_MEMORY;
     }
-    // (best effort: without it the automatic path choice keeps the coarse kernel)
-    if (hipHostMalloc(reinterpret_cast<void**>(&ctx->od_verdict), 64, hipHostMallocDefault) ==
-        hipSuccess)
+    // (best effort: without it the automatic path choice keeps the coarse
+    // kernel; without the coherent device mapping the verdict is copied)
+    if (hipHostMalloc(reinterpret_cast<void**>(&ctx->od_verdict), 64,
+                      RT_VERDICT_DIRECT ? hipHostMallocMapped | hipHostMallocCoherent
+                                        : hipHostMallocDefault) == hipSuccess) {
         *ctx->od_verdict = 0u;
-    else
+        void* dev = nullptr;
+        if (RT_VERDICT_DIRECT &&
+            hipHostGetDevicePointer(&dev, ctx->od_verdict, 0) == hipSuccess && dev)
+            ctx->od_verdict_dev = static_cast<unsigned*>(dev);
+    } else {
         ctx->od_verdict = nullptr;
+    }
     (void)hipGetLastError();
     // One-time setup here, as openCLInit builds the program before any trace
     // (MainState.cpp:1290-1320, outside the per-trace timer :662-894): every
@@ -561,10 +575,14 @@ void rt_destroy(rt_ctx* ctx) {
     // none may still be landing in the word (or reading flag) when it goes.
     // The context's event follows the last one; waiting for it (not for the
     // whole device) leaves other contexts' and other libraries' streams alone.
+    // (Direct verdict writes come from the frames' own kernels: hipHostFree
+    // below synchronises the device before it frees the word, as the HIP
+    // API documents, so no kernel still writes into it.)
     if (ctx->verdict_copies && ctx->verdict_done) (void)hipEventSynchronize(ctx->verdict_done);
     if (ctx->scene_stage) (void)hipHostFree(ctx->scene_stage);
     if (ctx->od_verdict) (void)hipHostFree(ctx->od_verdict);
     ctx->od_verdict = nullptr;
+    ctx->od_verdict_dev = nullptr;
     for (void* p : {ctx->scene_buf, ctx->origin_buf, ctx->out_buf, ctx->rec_buf, ctx->list_buf,
                     static_cast<void*>(ctx->flag)})
         if (p) (void)hipFree(p);
