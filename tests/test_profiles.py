@@ -257,7 +257,7 @@ def test_round6_rehearsal_lines_carry_the_scaling_contract():
             assert d["host_frame"][fmt]["frame_check"] == "bit-exact"
 
 
-@pytest.mark.parametrize("tag", ["r06k_final", "r06m_final", "r06s_final"])
+@pytest.mark.parametrize("tag", ["r06k_final", "r06m_final", "r06s_final", "r06v_final"])
 def test_round6_final_line_agrees_with_rocprof_and_pmc(tag):
     """The final round-6 lines (profiles/r06/bench_<tag>.json): the trace
     kernel's time from its packet events within 5 % of rocprofv3's mean over
