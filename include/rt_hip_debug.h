@@ -81,6 +81,14 @@ int rt_debug_set_coarse_waves(rt_ctx* ctx, int waves);
  * 4 frames for int32x4, 1 for RGBA8), 1 = wherever it applies, 2 = never. */
 int rt_debug_set_trace_bin(rt_ctx* ctx, int mode);
 
+/* How the overdraw verdict behind the automatic path choice reaches the
+ * host: 0 (default where the device can map the context's page-locked word)
+ * = the coarse kernel / trace_bin_kernel store it there themselves, every
+ * binned launch; 1 = they store it in device memory and a 4-byte copy every
+ * 8th binned launch brings it over (the library's fallback, and round 5's
+ * only way).  RT_ERR_UNSUPPORTED for 0 where the word is not mapped. */
+int rt_debug_set_verdict_copy(rt_ctx* ctx, int copy);
+
 /* The box overdraw of the last binned render of >= 1 band on this context
  * (prep's sum of the primitives' pixel-box areas over the band's area, in
  * frames; what the automatic path choices gate on).  Synchronises the

@@ -167,6 +167,7 @@ def library() -> ctypes.CDLL:
         "rt_debug_set_trace_split": (ctypes.c_int, [vp, ctypes.c_int]),
         "rt_debug_set_coarse_waves": (ctypes.c_int, [vp, ctypes.c_int]),
         "rt_debug_set_trace_bin": (ctypes.c_int, [vp, ctypes.c_int]),
+        "rt_debug_set_verdict_copy": (ctypes.c_int, [vp, ctypes.c_int]),
         "rt_debug_last_overdraw": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double)]),
         "rt_debug_triangle_t_bounds": (ctypes.c_int, [vp, vp, vp, vp, i32, i32, i32, i32, i32,
                                                       i32, i32, vp]),
@@ -590,6 +591,13 @@ class RayTracer:
         (default), 1 = wherever it applies, 2 = never (diagnostics / tests)."""
         _check(library().rt_debug_set_trace_bin(self._ctx, int(mode)),
                "rt_debug_set_trace_bin")
+
+    def set_verdict_copy(self, copy: bool) -> None:
+        """How the overdraw verdict reaches the host (rt_debug_set_verdict_copy):
+        False (default) = the kernels store it into the mapped host word,
+        True = a copy every 8th binned launch (the fallback; tests)."""
+        _check(library().rt_debug_set_verdict_copy(self._ctx, int(bool(copy))),
+               "rt_debug_set_verdict_copy")
 
     def last_overdraw(self) -> float:
         """rt_debug_last_overdraw: the last binned render's box overdraw, in

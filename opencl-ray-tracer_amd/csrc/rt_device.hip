@@ -159,6 +159,7 @@ struct rt_ctx {
     // rt_destroy after every write into it has landed.
     unsigned* od_verdict = nullptr;
     unsigned* od_verdict_dev = nullptr;  // its device mapping (direct writes), or null
+    unsigned* od_verdict_map = nullptr;  // the mapping, kept (rt_debug_set_verdict_copy)
     unsigned verdict_copies = 0;  // copies enqueued
     // recorded behind every verdict copy: rt_destroy waits for the last one
     // only (a context's renders move to another stream only after a
@@ -517,7 +518,7 @@ int rt_init(int device_ordinal, rt_ctx** out_ctx) {
         void* dev = nullptr;
         if (RT_VERDICT_DIRECT &&
             hipHostGetDevicePointer(&dev, ctx->od_verdict, 0) == hipSuccess && dev)
-            ctx->od_verdict_dev = static_cast<unsigned*>(dev);
+            ctx->od_verdict_dev = ctx->od_verdict_map = static_cast<unsigned*>(dev);
     } else {
         ctx->od_verdict = nullptr;
     }
@@ -582,7 +583,7 @@ void rt_destroy(rt_ctx* ctx) {
     if (ctx->scene_stage) (void)hipHostFree(ctx->scene_stage);
     if (ctx->od_verdict) (void)hipHostFree(ctx->od_verdict);
     ctx->od_verdict = nullptr;
-    ctx->od_verdict_dev = nullptr;
+    ctx->od_verdict_dev = ctx->od_verdict_map = nullptr;
     for (void* p : {ctx->scene_buf, ctx->origin_buf, ctx->out_buf, ctx->rec_buf, ctx->list_buf,
                     static_cast<void*>(ctx->flag)})
         if (p) (void)hipFree(p);
@@ -1034,6 +1035,13 @@ int rt_debug_last_overdraw(rt_ctx* ctx, double* frames) {
 int rt_debug_set_trace_bin(rt_ctx* ctx, int mode) {
     if (!ctx || mode < 0 || mode > 2) return RT_ERR_INVALID_ARG;
     ctx->trace_bin = mode;
+    return RT_OK;
+}
+
+int rt_debug_set_verdict_copy(rt_ctx* ctx, int copy) {
+    if (!ctx || copy < 0 || copy > 1) return RT_ERR_INVALID_ARG;
+    if (!copy && !ctx->od_verdict_map) return RT_ERR_UNSUPPORTED;
+    ctx->od_verdict_dev = copy ? nullptr : ctx->od_verdict_map;
     return RT_OK;
 }
 

@@ -985,6 +985,39 @@ def test_trace_bin_automatic_choice(pkg, oracle):
         assert np.array_equal(g1, want_sparse) and np.array_equal(g2, want_sparse)
 
 
+def test_verdict_copy_fallback(pkg, oracle):
+    """rt_debug_set_verdict_copy: the library's fallback where the device
+    cannot map the page-locked verdict word (the kernels store the verdict in
+    device memory, a 4-byte copy every 8th binned launch brings it over) still
+    picks the paths, later: a jump to high overdraw leaves trace_bin_kernel
+    within 8 frames; switched back to the kernels' own stores, the path
+    follows from the next frame.  Every frame is the oracle's."""
+    low = pkg.Scene.synthetic(2048, 2048, 256, 64, seed=3, k=3.2)
+    high = pkg.Scene.synthetic(2048, 2048, 256, 64, seed=3, k=12.8)
+    want_low = oracle.trace(low, 2048, 2048, threads=THREADS)
+    want_high = oracle.trace(high, 2048, 2048, threads=THREADS)
+    with pkg.RayTracer(0) as rt:
+        rt.set_verdict_copy(True)
+        kernels = []
+        for scene, want, n in ((low, want_low, 2), (high, want_high, 10)):
+            for _ in range(n):
+                f, _ = rt.render(scene, 2048, 2048)
+                kernels.append(rt.last_kernel())
+                assert np.array_equal(f, want), kernels
+        assert kernels[:3] == ["trace3_kernel", "trace_bin_kernel", "trace_bin_kernel"], kernels
+        assert 3 < kernels.index("trace3_kernel", 2) <= 10, kernels
+        assert kernels[-1] == "trace3_kernel", kernels
+        rt.set_verdict_copy(False)
+        kernels = []
+        for _ in range(4):
+            f, _ = rt.render(low, 2048, 2048)
+            kernels.append(rt.last_kernel())
+            assert np.array_equal(f, want_low), kernels
+        assert kernels == ["trace3_kernel"] + ["trace_bin_kernel"] * 3, kernels
+    lib = pkg.library()
+    assert lib.rt_debug_set_verdict_copy(None, 0) == -1  # RT_ERR_INVALID_ARG
+
+
 def test_last_kernel_names_the_path_taken(pkg, rt, oracle):
     """rt_last_kernel reports the kernel that actually ran (the bench's
     `kernel` label): frame_small_kernel for <= 128 primitives on a resident
