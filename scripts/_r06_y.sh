@@ -1,7 +1,8 @@
 #!/bin/bash
 # Round 6: the host's wait in the timed regions.  The bench with
 # hipDeviceScheduleSpin (--sync-wait spin, the new default) against HIP's
-# default wait, interleaved, three rounds; then scripts/window_fill.py (the
+# default wait, interleaved, three rounds (--sync-wait existed in bench.py
+# while this was measured; not kept); then scripts/window_fill.py (the
 # K-window's fixed cost and per-frame completion times) under spin.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
