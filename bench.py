@@ -116,9 +116,10 @@ def parse(argv=None):
                          "torch's pool (round 5: RGBA8 3 slots 39.5-40.0 us per frame on hip "
                          "streams, 33.0 on cumask, 32.8-33.8 on torch's; int32x4 2 slots "
                          "51.1-52.0 on all three, profiles/r05/slot_streams.txt)")
-    ap.add_argument("--inflight-rgba8", type=int, default=3,
+    ap.add_argument("--inflight-rgba8", type=int, default=4,
                     help="the same for the texture_rgba8 leg (its trace leaves more room "
-                         "beside it: 3 slots measured best, DESIGN.md §3.4)")
+                         "beside it: 4 slots measured best on the round-6 library, "
+                         "DESIGN.md §3.4)")
     ap.add_argument("--pg-timeout", type=float, default=60.0,
                     help="N>1: seconds before a data-path collective that another rank left "
                          "unmatched raises (gloo) or has its communicator aborted (RCCL, "
